@@ -1,0 +1,90 @@
+"""ctypes binding of libmpcqp.so (include/mpcqp.h).
+
+The shared library is built in-tree (``__graft_entry__.build()`` or
+``python -m mpcqp.build``) next to this file.  There is deliberately no
+fallback: if the library is missing or fails to load, every entry point raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmpcqp.so")
+
+MPCQP_OK = 0
+STATUS_OK = 0
+STATUS_MAX_ITER = 1
+STATUS_INFEASIBLE = 2
+STATUS_TOO_LARGE = 3
+STATUS_NONFINITE = 4
+ROBOT_STRIDE = 16
+
+# every symbol declared in include/mpcqp.h
+EXPORTED_SYMBOLS = (
+    "mpcqp_abi_version",
+    "mpcqp_default_params",
+    "mpcqp_create",
+    "mpcqp_solve",
+    "mpcqp_set_stance_hint",
+    "mpcqp_destroy",
+    "mpcqp_last_error",
+)
+
+
+class MpcqpParams(ctypes.Structure):
+    """struct mpcqp_params (include/mpcqp.h)."""
+    _fields_ = [
+        ("horizon", ctypes.c_int32),
+        ("max_iter", ctypes.c_int32),
+        ("dt", ctypes.c_double),
+        ("q_diag", ctypes.c_double * 13),
+        ("r_diag", ctypes.c_double * 12),
+    ]
+
+
+class MpcqpError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load libmpcqp.so once; raise MpcqpError if it is absent (no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MpcqpError(f"{LIB_PATH} not built: run __graft_entry__.build() "
+                         "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, i32, f32p, i32p = ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p
+    lib.mpcqp_abi_version.restype = i32
+    lib.mpcqp_abi_version.argtypes = []
+    lib.mpcqp_default_params.restype = None
+    lib.mpcqp_default_params.argtypes = [ctypes.POINTER(MpcqpParams), i32]
+    lib.mpcqp_create.restype = ctypes.c_int
+    lib.mpcqp_create.argtypes = [ctypes.POINTER(MpcqpParams), i32, ctypes.POINTER(vp)]
+    lib.mpcqp_solve.restype = ctypes.c_int
+    lib.mpcqp_solve.argtypes = [vp, i32, f32p, f32p, f32p, f32p, f32p, f32p, f32p, i32p, i32p, vp]
+    lib.mpcqp_set_stance_hint.restype = ctypes.c_int
+    lib.mpcqp_set_stance_hint.argtypes = [vp, i32]
+    lib.mpcqp_destroy.restype = ctypes.c_int
+    lib.mpcqp_destroy.argtypes = [vp]
+    lib.mpcqp_last_error.restype = ctypes.c_char_p
+    lib.mpcqp_last_error.argtypes = [vp]
+    if lib.mpcqp_abi_version() != 1:
+        raise MpcqpError("libmpcqp ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def default_params(horizon):
+    p = MpcqpParams()
+    load().mpcqp_default_params(ctypes.byref(p), int(horizon))
+    return p
+
+
+def check(ctx, code, what):
+    if code != MPCQP_OK:
+        msg = load().mpcqp_last_error(ctx) if ctx else b""
+        raise MpcqpError(f"{what} failed ({code}): {msg.decode() if msg else ''}")

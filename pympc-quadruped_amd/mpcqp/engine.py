@@ -1,0 +1,156 @@
+"""Batched convex-MPC QP engine (host side).
+
+``LinearMpc(...).solve(state, xref, contact_schedule, feet=...)`` formulates
+and solves B independent reference MPC QPs in one HIP launch and returns the
+first-step ground-reaction forces u0[B, 12] -- the batched form of
+``ModelPredictiveController._solve_mpc(...)[0:12]``
+(/root/reference/linear_mpc/mpc.py:262-290, :99).
+
+torch-ROCm tensors are storage only: inputs are moved (zero-copy when they are
+already contiguous float32 tensors on the engine's device) and the compute is
+the HIP kernel behind ``libmpcqp.so`` (include/mpcqp.h).  There is no CPU path.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .params import (DT_MPC, Q_DIAG, R_DIAG, ROBOT_PRESETS, ROBOT_STRIDE, pack_robot)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+class SolveResult:
+    """u0[B,12] plus optional U[B,N,12], status[B], iterations[B] (device tensors)."""
+
+    def __init__(self, u0, U, status, iters):
+        self.u0, self.U, self.status, self.iterations = u0, U, status, iters
+
+
+class LinearMpc:
+    """Batched reference MPC: one QP per robot, solved on one MI355X.
+
+    Args:
+      horizon:  N (LinearMpcConfig.horizon, config/linear_mpc_configs.py:11)
+      robot:    default per-robot parameters: a preset name ("a1", "aliengo"),
+                a reference RobotConfig class, or a packed [16] record.
+      dt:       model step (hard-coded 0.05 in mpc.py:38)
+      Q, R:     diagonal weights (linear_mpc_configs.py:19-20)
+      device:   torch device of the HIP context (default cuda:0)
+      max_iter: active-set iteration cap per robot (0 = engine default)
+      max_stance: optional promise of at most this many stance foot-steps per
+                robot (lets the engine skip larger capacity classes)
+    """
+
+    def __init__(self, horizon=16, robot="aliengo", dt=DT_MPC, Q=Q_DIAG, R=R_DIAG,
+                 device="cuda:0", max_iter=0, max_stance=0):
+        self.horizon = int(horizon)
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("LinearMpc runs on a HIP device only (no CPU path)")
+        self.lib = _lib.load()
+        p = _lib.default_params(self.horizon)
+        p.dt = float(dt)
+        p.max_iter = int(max_iter)
+        for i, v in enumerate(np.asarray(Q, dtype=np.float64).reshape(-1)):
+            p.q_diag[i] = float(v)
+        for i, v in enumerate(np.asarray(R, dtype=np.float64).reshape(-1)):
+            p.r_diag[i] = float(v)
+        self.params = p
+        ctx = ctypes.c_void_p()
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        _lib.check(None, self.lib.mpcqp_create(ctypes.byref(p), int(idx), ctypes.byref(ctx)),
+                   "mpcqp_create")
+        self._ctx = ctx
+        if max_stance:
+            _lib.check(ctx, self.lib.mpcqp_set_stance_hint(ctx, int(max_stance)), "set_stance_hint")
+        self.default_robot = self._robot_record(robot)
+
+    def __del__(self):
+        ctx = getattr(self, "_ctx", None)
+        if ctx is not None and ctx.value:
+            try:
+                self.lib.mpcqp_destroy(ctx)
+            except Exception:
+                pass
+            self._ctx = None
+
+    @staticmethod
+    def _robot_record(robot):
+        if robot is None:
+            return None
+        if isinstance(robot, str):
+            return pack_robot(ROBOT_PRESETS[robot])
+        if hasattr(robot, "mass_base"):
+            from .params import robot_from_config
+            return robot_from_config(robot)
+        rec = np.asarray(robot, dtype=np.float32).reshape(-1)
+        if rec.shape[0] != ROBOT_STRIDE:
+            raise ValueError(f"robot record must have {ROBOT_STRIDE} entries")
+        return rec
+
+    def _dev(self, a, shape, name):
+        t = torch.as_tensor(a)
+        t = t.to(device=self.device, dtype=torch.float32).contiguous()
+        if tuple(t.shape) != tuple(shape):
+            try:
+                t = t.reshape(shape)
+            except RuntimeError:
+                raise ValueError(f"{name}: expected shape {shape}, got {tuple(t.shape)}")
+        return t
+
+    def solve(self, state, xref, contact_schedule, feet, robot=None, return_all=False, stream=None):
+        """Formulate + solve B QPs.
+
+        state:            [B,13] x0 (mpc.py:65-77) -- x0[2] is the yaw of the model
+        xref:             [B,N,13] or [B,13N] reference (mpc.py:154-168)
+        contact_schedule: [B,N,4] or [B,4N] gait table (gait.py:81-100)
+        feet:             [B,4,3] foot positions relative to the CoM, world frame
+        robot:            [B,16] per-robot records, or one record / preset for all
+        Returns u0 [B,12] (device tensor), or a SolveResult if return_all.
+        """
+        st = torch.as_tensor(state)
+        B = int(st.shape[0]) if st.dim() == 2 else 1
+        N = self.horizon
+        x0 = self._dev(state, (B, 13), "state")
+        xr = self._dev(xref, (B, N, 13), "xref")
+        ct = self._dev(contact_schedule, (B, N, 4), "contact_schedule")
+        ft = self._dev(feet, (B, 4, 3), "feet")
+        if robot is None:
+            if self.default_robot is None:
+                raise ValueError("no robot parameters")
+            rb = torch.as_tensor(np.tile(self.default_robot, (B, 1)))
+        else:
+            r = robot if not isinstance(robot, str) and not hasattr(robot, "mass_base") else None
+            if r is None:
+                rb = torch.as_tensor(np.tile(self._robot_record(robot), (B, 1)))
+            else:
+                rt = torch.as_tensor(r)
+                rb = rt.reshape(1, -1).expand(B, -1) if rt.dim() == 1 else rt
+        rb = self._dev(rb, (B, ROBOT_STRIDE), "robot")
+        u0 = torch.empty((B, 12), dtype=torch.float32, device=self.device)
+        U = torch.empty((B, N, 12), dtype=torch.float32, device=self.device) if return_all else None
+        status = torch.empty((B,), dtype=torch.int32, device=self.device)
+        iters = torch.empty((B,), dtype=torch.int32, device=self.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        code = self.lib.mpcqp_solve(self._ctx, B, _ptr(x0), _ptr(xr), _ptr(ct), _ptr(ft), _ptr(rb),
+                                    _ptr(u0), _ptr(U), _ptr(status), _ptr(iters),
+                                    ctypes.c_void_p(stream.cuda_stream))
+        _lib.check(self._ctx, code, "mpcqp_solve")
+        if return_all:
+            return SolveResult(u0, U, status, iters)
+        return u0
+
+    def solve_raw(self, B, x0, xref, contact, feet, robot, u0, U=None, status=None, iters=None,
+                  stream=None):
+        """Zero-overhead launch on preallocated contiguous float32 device tensors."""
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        code = self.lib.mpcqp_solve(self._ctx, int(B), _ptr(x0), _ptr(xref), _ptr(contact),
+                                    _ptr(feet), _ptr(robot), _ptr(u0), _ptr(U), _ptr(status),
+                                    _ptr(iters), ctypes.c_void_p(stream.cuda_stream))
+        _lib.check(self._ctx, code, "mpcqp_solve")
