@@ -1,0 +1,219 @@
+"""bench.py -- QP solves/sec of the MI355X batched MPC engine (BASELINE.json metric).
+
+  python bench.py --gpus N --steps K --warmup W
+  (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL backend)
+
+Workload (BASELINE.json configs[1]): per GPU B = 1024 A1 robots, trotting
+(trot10), horizon N = 10, synthetic seeded states; weak scaling
+(B per GPU is fixed as N grows).  One step = one pass of the hot path over the
+batch: formulate (model, exact discretisation, condensing, H/g, cone rows) and
+solve every robot's QP, plus -- on N > 1 -- the end-of-step RCCL all-gather of
+u0 (the only exchange the path has).  Inputs are resident in HBM before the
+timed region.
+
+Prints ONE JSON line on rank 0 (metric/value/unit/... + roofline + cpu_baseline).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "pympc-quadruped_amd"))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (batch per GPU, horizon, gaits, robots, tilt)
+    "config2": (1024, 10, ("trot10",), ("a1",), 0.0),
+    "config3": (4096, 10, ("trot10", "pace10", "bound8"), ("a1",), 0.0),
+    "config4": (2048, 16, ("trot10", "pace10", "bound8"), ("a1",), 0.0),
+    "config5": (8192, 20, ("trot10", "pace10", "bound8"), ("a1", "aliengo"), 15.0),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="config2", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=0, help="override batch per GPU")
+    ap.add_argument("--no-gather", action="store_true", help="skip the end-of-step u0 gather")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(bt, N, budget_s):
+    """Reference-faithful NumPy formulation + exact float64 QP solve, 1 core."""
+    try:
+        from threadpoolctl import threadpool_limits
+        lim = threadpool_limits(1)
+    except Exception:
+        lim = None
+    from oracle import formulation as F
+    from oracle import qp as Q
+    import numpy as np
+    B = bt["x0"].shape[0]
+    t0 = time.perf_counter()
+    done = 0
+    for b in range(B):
+        rec = bt["robot"][b]
+        inertia = np.array([[rec[1], rec[2], rec[3]], [rec[2], rec[4], rec[5]],
+                            [rec[3], rec[5], rec[6]]], dtype=np.float32)
+        o = F.formulate(bt["x0"][b], bt["xref"][b].reshape(-1), bt["contact"][b].reshape(-1),
+                        bt["feet"][b].astype(np.float64), inertia, float(rec[0]), N,
+                        mu=float(rec[7]), fz_max=float(rec[8]))
+        Q.solve_qp_dual_active_set(o["H"], o["g"], o["C"], o["lb"], o["ub"])
+        done += 1
+        if time.perf_counter() - t0 > budget_s and done >= 3:
+            break
+    dt = time.perf_counter() - t0
+    if lim is not None:
+        lim.unregister() if hasattr(lim, "unregister") else None
+    return done / dt, done, dt
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from mpcqp import LinearMpc
+    from mpcqp.synthetic import make_batch
+    from mpcqp.roofline import PEAK_FP64_TFLOPS, algorithmic_flops, executed_flops
+
+    Bpg, N, gaits, robots, tilt = CONFIGS[args.config]
+    if args.batch:
+        Bpg = args.batch
+    # a few distinct seeded batches per rank, cycled over the steps (seed = base + rank)
+    nbat = 4
+    host = [make_batch(Bpg, N, seed=1000 * (k + 1) + rank, gaits=gaits, robots=robots, tilt_deg=tilt)
+            for k in range(nbat)]
+    eng = LinearMpc(horizon=N, robot=robots[0], device=dev)
+    dev_b = []
+    for h in host:
+        dev_b.append({k: torch.as_tensor(v).to(dev).contiguous() for k, v in h.items()})
+    u0 = torch.empty((Bpg, 12), dtype=torch.float32, device=dev)
+    status = torch.empty((Bpg,), dtype=torch.int32, device=dev)
+    iters = [torch.empty((Bpg,), dtype=torch.int32, device=dev) for _ in range(nbat)]
+    gathered = torch.empty((world * Bpg, 12), dtype=torch.float32, device=dev) if world > 1 else None
+    stream = torch.cuda.current_stream(dev)
+
+    def step(k, ev=None):
+        d = dev_b[k % nbat]
+        if ev is not None:
+            ev[0].record(stream)
+        eng.solve_raw(Bpg, d["x0"], d["xref"], d["contact"], d["feet"], d["robot"], u0,
+                      None, status, iters[k % nbat], stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+        if gathered is not None and not args.no_gather:
+            dist.all_gather_into_tensor(gathered, u0)
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(k, events[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in events]
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    elapsed = float(tmax.item())
+
+    # algorithmic work per launch: per-robot n_eff and executed iterations
+    flops_launch = []
+    exec_launch = []
+    it_all = []
+    for k in range(nbat):
+        it = iters[k].cpu().numpy()
+        ns = 3 * (host[k]["contact"] > 0).reshape(Bpg, -1).sum(1)
+        flops_launch.append(sum(algorithmic_flops(N, int(n), int(i)) for n, i in zip(ns, it)))
+        exec_launch.append(sum(executed_flops(N, int(n), int(i)) for n, i in zip(ns, it)))
+        it_all.append(it)
+    st = status.cpu().numpy()
+    steps_per_bat = [sum(1 for s in range(args.steps) if s % nbat == k) for k in range(nbat)]
+    F_avg = sum(f * c for f, c in zip(flops_launch, steps_per_bat)) / args.steps
+    E_avg = sum(f * c for f, c in zip(exec_launch, steps_per_bat)) / args.steps
+    kavg_s = sum(kern_ms) / len(kern_ms) / 1e3
+    achieved = F_avg / kavg_s / 1e12
+    it_all = np.concatenate(it_all)
+
+    qps = world * Bpg * args.steps / elapsed
+    traffic = None
+    try:
+        with open(args.pmc_file) as fh:
+            pmc = json.load(fh)
+        entry = pmc.get(args.config)
+        if entry and entry.get("batch") == Bpg:
+            traffic = entry.get("hbm_bytes_per_launch")
+    except Exception:
+        traffic = None
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            v, done, dt = cpu_baseline(host[0], N, args.cpu_seconds)
+            cpu = {"value": v, "unit": "QP/s", "cores": 1, "kind": "port",
+                   "sample": f"{done} robots of the config's first synthetic batch in {dt:.1f}s: "
+                             "reference-faithful NumPy formulation (oracle/formulation.py) + "
+                             "exact float64 dual active-set QP (oracle/qp.py), 1 thread"}
+        line = {
+            "metric": "QP solves/sec (whole node), horizon=10 GRF QP, at 1/2/4/8 MI355X",
+            "value": qps,
+            "unit": "QP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded SURVEY §8(d) states, gait tables, feet; seed = base + rank)",
+            "config": {"workload": f"{args.config}: batch {Bpg}/GPU, horizon {N}, gaits {'+'.join(gaits)}, "
+                                   f"robots {'+'.join(robots)}" + (f", cone tilt <= {tilt} deg" if tilt else ""),
+                       "batch_per_gpu": Bpg, "horizon": N, "global_batch": world * Bpg,
+                       "parallelism": f"robot-sharded x{world}" + ("" if world == 1 or args.no_gather
+                                                                   else " + RCCL all-gather of u0")},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP64_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic},
+            "cpu_baseline": cpu,
+            "kernel_ms_avg": kavg_s * 1e3,
+            "executed_tflops": E_avg / kavg_s / 1e12,
+            "iters_mean": float(it_all.mean()),
+            "iters_max": int(it_all.max()),
+            "status_ok_frac": float((st == 0).mean()),
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,188 @@
+"""Generate the golden fixtures in tests/golden/ FROM THE REFERENCE ITSELF.
+
+Runs only in the build container (it reads /root/reference, which never
+travels to the GPU box).  The reference's formulation functions are imported
+with the four unavailable third-party modules stubbed (numba, pydrake,
+qpsolvers, pinocchio -- none of them is called on the formulation path;
+SURVEY.md Appendix A), then:
+
+  formulation_N{N}.npz  inputs + the reference's own (H, g) for every case,
+                        (C, lb, ub) for the first cases, and u* = the exact
+                        optimum of the reference-built QP (oracle/qp.py dual
+                        active set, float64) with its KKT residuals.
+  gait_N{N}.npz         Gait.get_gait_table() (linear_mpc/gait.py:81-100) for
+                        every gait member and iterations 0..2*period
+  reftraj.npz           generate_reference_trajectory() (mpc.py:110-170) and
+                        the update_mpc_if_needed pose integration (mpc.py:83-92)
+
+Usage:  python tests/golden/make_golden.py            (all horizons, subprocesses)
+        python tests/golden/make_golden.py --horizon 10
+"""
+import argparse
+import os
+import subprocess
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+HORIZONS = (10, 16, 20)
+
+
+def stub_reference(horizon):
+    sys.path[:0] = [f"{REF}/linear_mpc", f"{REF}/config", f"{REF}/utils"]
+    nb = types.ModuleType("numba")
+    nb.jit = lambda *a, **k: (lambda f: f)
+    nb.vectorize = nb.jit
+    nb.float32 = np.float32
+    pda = types.ModuleType("pydrake.all")
+    pda.MathematicalProgram = pda.Solve = pda.PiecewisePolynomial = None
+    pd = types.ModuleType("pydrake")
+    pd.all = pda
+    qs = types.ModuleType("qpsolvers")
+    qs.solve_qp = None
+    sys.modules.update({"numba": nb, "pydrake": pd, "pydrake.all": pda, "qpsolvers": qs,
+                        "pinocchio": types.ModuleType("pinocchio")})
+    import linear_mpc_configs
+    # Gait captures the horizon when the Enum is created (gait.py:47-50): set it first
+    linear_mpc_configs.LinearMpcConfig.horizon = horizon
+    import gait
+    import mpc
+    import robot_configs
+    return linear_mpc_configs.LinearMpcConfig, robot_configs, mpc, gait
+
+
+def gen(horizon):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "pympc-quadruped_amd")]
+    LinearMpcConfig, robot_configs, mpc, gait = stub_reference(horizon)
+    from oracle import qp as Q
+    from mpcqp.synthetic import make_batch
+    from mpcqp.params import robot_from_config
+
+    N = horizon
+    cfgs = {"a1": robot_configs.A1Config, "aliengo": robot_configs.AliengoConfig}
+    gaits = ("trot10", "pace10", "bound8", "standing")
+    names = ("a1", "aliengo")
+    B = 16
+    bt = make_batch(B, N, seed=4242 + N, gaits=gaits, robots=names)
+    # per-robot records straight from the reference config classes
+    robot_name = []
+    for b in range(B):
+        nm = "a1" if abs(bt["robot"][b][0] - 4.713) < 1e-3 else "aliengo"
+        robot_name.append(nm)
+        bt["robot"][b] = robot_from_config(cfgs[nm])
+    Hs, gs, us, kkts, iters = [], [], [], [], []
+    C0 = lb0 = ub0 = None
+    Cs, lbs, ubs = [], [], []
+    for b in range(B):
+        c = mpc.ModelPredictiveController(LinearMpcConfig, cfgs[robot_name[b]])
+        x0 = bt["x0"][b].copy()
+        c.current_state = x0
+        c.yaw = float(x0[2])
+        c.pos_base_feet = [bt["feet"][b][i].astype(np.float64) for i in range(4)]
+        Ac, Bc = c._generate_state_space_model()
+        c._discretize_continuous_model(Ac, Bc)
+        Ad, Bd = c._discretize_continuous_model(Ac, Bc)
+        H, g = c._generate_QP_cost(Ad, Bd, c.current_state, bt["xref"][b].reshape(-1))
+        C, lb, ub = c._generate_QP_constraints(bt["contact"][b].reshape(-1))
+        x, y, info = Q.solve_qp_dual_active_set(H, g, C, lb, ub)
+        k = Q.kkt_residuals(H, g, C, lb, ub, x, y)
+        Hs.append(H)
+        gs.append(g)
+        us.append(x)
+        kkts.append([k["stationarity"], k["primal"], k["dual"], k["complementarity"]])
+        iters.append(info["iterations"])
+        if b < 2:
+            Cs.append(C); lbs.append(lb); ubs.append(ub)
+    # full H only for the first cases (size); every case keeps H @ probe vectors,
+    # a size-independent pin of the whole matrix
+    nH = 2 if N <= 16 else 1
+    probe = np.random.default_rng(99).standard_normal((2, 12 * N))
+    probe[0] = 1.0
+    Hprobe = np.array([[H @ v for v in probe] for H in Hs])
+    out = dict(x0=bt["x0"], xref=bt["xref"], contact=bt["contact"], feet=bt["feet"], robot=bt["robot"],
+               robot_name=np.array(robot_name), H=np.array(Hs[:nH]), H_probe=Hprobe, probe=probe,
+               g=np.array(gs), u_star=np.array(us),
+               kkt=np.array(kkts), iterations=np.array(iters), C=np.array(Cs), lb=np.array(lbs),
+               ub=np.array(ubs), horizon=N, dt=0.05)
+    np.savez_compressed(os.path.join(HERE, f"formulation_N{N}.npz"), **out)
+
+    # gait tables (linear_mpc/gait.py:16-22, :76-100)
+    tables = {}
+    for member in gait.Gait:
+        rows = []
+        for it in range(0, 2 * member.num_segment * 20 + 1, 20):
+            member.set_iteration(20, it)
+            rows.append(member.get_gait_table().copy())
+        tables[member.name] = np.array(rows)
+    np.savez_compressed(os.path.join(HERE, f"gait_N{N}.npz"), **tables)
+
+    if N == 16:
+        gen_reftraj(LinearMpcConfig, robot_configs, mpc)
+    print(f"N={N}: max KKT {np.array(kkts).max():.2e}, iterations {iters}")
+
+
+class _FakeRobotData:
+    def __init__(self, R):
+        self.R_base = R
+
+
+def gen_reftraj(LinearMpcConfig, robot_configs, mpc):
+    """generate_reference_trajectory + update_mpc_if_needed integrators (mpc.py:81-170)."""
+    rng = np.random.default_rng(77)
+    cases = []
+    for k in range(12):
+        c = mpc.ModelPredictiveController(LinearMpcConfig, robot_configs.AliengoConfig)
+        x0 = np.zeros(13, dtype=np.float32)
+        x0[:3] = rng.uniform(-0.1, 0.1, 3)
+        x0[2] = rng.uniform(-3, 3)
+        x0[3:6] = [rng.uniform(-1, 1), rng.uniform(-1, 1), 0.38]
+        x0[9:12] = [rng.uniform(-0.5, 1.5), rng.uniform(-0.3, 0.3), 0.0]
+        x0[12] = -9.81
+        c.current_state = x0
+        c.yaw = float(x0[2])
+        c.roll_init, c.pitch_init = 0.0, 0.0
+        c.is_initialized = True
+        yaw = float(x0[2])
+        R = np.array([[np.cos(yaw), -np.sin(yaw), 0], [np.sin(yaw), np.cos(yaw), 0], [0, 0, 1]])
+        c._ModelPredictiveController__robot_data = _FakeRobotData(R)
+        v_body = np.array([rng.uniform(0, 1.5), 0.0, 0.0])
+        yaw_rate = float(rng.uniform(-0.5, 0.5))
+        # run the integrators for a few ticks (iteration_between_mpc = 20, so no solve
+        # is triggered except at multiples of 20 -- we call the pieces directly)
+        seq = []
+        for tick in range(3):
+            vel_des = c._ModelPredictiveController__robot_data.R_base @ v_body
+            if c.is_first_run:
+                c.xpos_base_desired, c.ypos_base_desired, c.yaw_desired = 0.0, 0.0, c.yaw
+                c.is_first_run = False
+            else:
+                c.xpos_base_desired += c.dt_control * vel_des[0]
+                c.ypos_base_desired += c.dt_control * vel_des[1]
+                c.yaw_desired = c.yaw + c.dt_control * yaw_rate
+            X = c.generate_reference_trajectory(vel_des, yaw_rate)
+            seq.append(X.copy())
+        cases.append(dict(x0=x0, v_body=v_body, yaw_rate=yaw_rate, R=R, X=np.array(seq),
+                          roll_init=c.roll_init, pitch_init=c.pitch_init))
+    np.savez_compressed(os.path.join(HERE, "reftraj.npz"),
+                        x0=np.array([c_["x0"] for c_ in cases]),
+                        v_body=np.array([c_["v_body"] for c_ in cases]),
+                        yaw_rate=np.array([c_["yaw_rate"] for c_ in cases]),
+                        R=np.array([c_["R"] for c_ in cases]),
+                        X=np.array([c_["X"] for c_ in cases]),
+                        roll_init=np.array([c_["roll_init"] for c_ in cases]),
+                        pitch_init=np.array([c_["pitch_init"] for c_ in cases]))
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--horizon", type=int, default=0)
+    a = ap.parse_args()
+    if a.horizon:
+        gen(a.horizon)
+    else:
+        for n in HORIZONS:
+            subprocess.run([sys.executable, __file__, "--horizon", str(n)], check=True)
