@@ -1,0 +1,56 @@
+"""Diagnostic: per-phase cycle shares of the engine kernel (s_memtime stamps).
+
+Uses a separately built libmpcqp_stamps.so (-DMPCQP_STAMPS) whose kernel writes
+7 timestamps per robot into the U buffer; the shipped library executes no stamp.
+Prints median / max cycles per phase over the batch.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "pympc-quadruped_amd"))
+from mpcqp import _lib  # noqa: E402
+from mpcqp.synthetic import make_batch  # noqa: E402
+
+PHASES = ["inputs+model+discretise", "g,Y,T", "H rows", "sweep H^-1", "active set", "refine+verify"]
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+    N = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    _lib.LIB_PATH = os.path.join(ROOT, "pympc-quadruped_amd", "mpcqp", "libmpcqp_stamps.so")
+    lib = _lib.load()
+    p = _lib.default_params(N)
+    ctx = ctypes.c_void_p()
+    _lib.check(None, lib.mpcqp_create(ctypes.byref(p), 0, ctypes.byref(ctx)), "create")
+    bt = make_batch(B, N, seed=1000, gaits=("trot10",), robots=("a1",))
+    dev = torch.device("cuda:0")
+    d = {k: torch.as_tensor(v).to(dev).contiguous() for k, v in bt.items()}
+    u0 = torch.empty((B, 12), device=dev)
+    U = torch.zeros((B, N, 12), device=dev)
+    st = torch.empty((B,), dtype=torch.int32, device=dev)
+    it = torch.empty((B,), dtype=torch.int32, device=dev)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    for _ in range(3):
+        lib.mpcqp_solve(ctx, B, P(d["x0"]), P(d["xref"]), P(d["contact"]), P(d["feet"]), P(d["robot"]),
+                        P(u0), P(U), P(st), P(it), ctypes.c_void_p(0))
+    torch.cuda.synchronize()
+    ts = U.cpu().numpy().reshape(B, -1).view(np.uint64)[:, :7].astype(np.int64)
+    dts = np.diff(ts, axis=1)
+    iters = it.cpu().numpy()
+    print(f"B={B} N={N}  iterations mean {iters.mean():.1f} max {iters.max()}")
+    for k, name in enumerate(PHASES):
+        print(f"  {name:26s} median {np.median(dts[:, k]):9.0f}  max {dts[:, k].max():9.0f} cycles")
+    tot = ts[:, 6] - ts[:, 0]
+    print(f"  {'total':26s} median {np.median(tot):9.0f}  max {tot.max():9.0f}")
+    gi = dts[:, 4]
+    sel = iters > 0
+    print(f"  active-set cycles / iteration: median {np.median(gi[sel] / iters[sel]):.0f}")
+
+
+if __name__ == "__main__":
+    main()
