@@ -93,6 +93,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from mpcqp import LinearMpc
+    from mpcqp.dist import gather_u0
     from mpcqp.synthetic import make_batch
     from mpcqp.roofline import PEAK_FP64_TFLOPS, algorithmic_flops, executed_flops
 
@@ -110,7 +111,6 @@ def main():
     u0 = torch.empty((Bpg, 12), dtype=torch.float32, device=dev)
     status = torch.empty((Bpg,), dtype=torch.int32, device=dev)
     iters = [torch.empty((Bpg,), dtype=torch.int32, device=dev) for _ in range(nbat)]
-    gathered = torch.empty((world * Bpg, 12), dtype=torch.float32, device=dev) if world > 1 else None
     stream = torch.cuda.current_stream(dev)
 
     def step(k, ev=None):
@@ -121,8 +121,8 @@ def main():
                       None, status, iters[k % nbat], stream=stream)
         if ev is not None:
             ev[1].record(stream)
-        if gathered is not None and not args.no_gather:
-            dist.all_gather_into_tensor(gathered, u0)
+        if world > 1 and not args.no_gather:
+            gather_u0(u0)
 
     for k in range(args.warmup):
         step(k)

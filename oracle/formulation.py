@@ -127,12 +127,26 @@ def condensed_cost(Ad, Bd, x0, xref, horizon, q_diag=Q_DIAG, r_diag=R_DIAG):
     return H, g, Su, Sx
 
 
-def friction_constraints(contact, horizon, mu=MU, fz_max=500.0):
+def cone_rows(mu, normal=None):
+    """Friction-pyramid rows.  normal=None (or e_z) is exactly mpc.py:239-245;
+    a unit normal n gives [t1+mu n, -t1+mu n, t2+mu n, -t2+mu n, n] with
+    t1 = normalise(e_x - n_x n), t2 = n x t1 (build-only generalisation)."""
+    if normal is None or np.array_equal(np.asarray(normal, dtype=np.float64), (0.0, 0.0, 1.0)):
+        return np.array([[1, 0, mu], [-1, 0, mu], [0, 1, mu], [0, -1, mu], [0, 0, 1]],
+                        dtype=np.float32)
+    n = np.asarray(normal, dtype=np.float64)
+    n = n / np.linalg.norm(n)
+    t1 = np.array([1.0, 0.0, 0.0]) - n[0] * n
+    t1 /= np.linalg.norm(t1)
+    t2 = np.cross(n, t1)
+    return np.array([t1 + mu * n, -t1 + mu * n, t2 + mu * n, -t2 + mu * n, n])
+
+
+def friction_constraints(contact, horizon, mu=MU, fz_max=500.0, normal=None):
     """mpc.py:237-260 -- C = kron(I_4N, cone), lb = 0, ub = [inf x4, contact*fz_max]."""
-    cone = np.array([[1, 0, mu], [-1, 0, mu], [0, 1, mu], [0, -1, mu], [0, 0, 1]],
-                    dtype=np.float32)
+    cone = cone_rows(mu, normal)
     N = horizon
-    C = np.kron(np.identity(4 * N, dtype=np.float32), cone)
+    C = np.kron(np.identity(4 * N, dtype=cone.dtype), cone)
     lb = np.zeros(20 * N, dtype=np.float32)
     ub = np.zeros(20 * N, dtype=np.float32)
     for k in range(4 * N):
@@ -142,7 +156,7 @@ def friction_constraints(contact, horizon, mu=MU, fz_max=500.0):
 
 
 def formulate(x0, xref, contact, feet, inertia, mass, horizon, mu=MU, fz_max=500.0,
-              dt=DT_MPC, yaw=None):
+              dt=DT_MPC, yaw=None, normal=None):
     """The whole formulation half of mpc.py:262-275 for one robot.
 
     ``yaw`` defaults to x0[2] (mpc.py:77 stores rpy[2] both in the state and in
@@ -155,5 +169,5 @@ def formulate(x0, xref, contact, feet, inertia, mass, horizon, mu=MU, fz_max=500
     Ac, Bc = continuous_model(yaw, np.asarray(inertia, dtype=np.float32), mass, feet)
     Ad, Bd = discretize(Ac, Bc, dt)
     H, g, _, _ = condensed_cost(Ad, Bd, x0, xref, horizon)
-    C, lb, ub = friction_constraints(np.asarray(contact).reshape(-1), horizon, mu, fz_max)
+    C, lb, ub = friction_constraints(np.asarray(contact).reshape(-1), horizon, mu, fz_max, normal)
     return dict(H=H, g=g, C=C, lb=lb, ub=ub, Ad=Ad, Bd=Bd, Ac=Ac, Bc=Bc)

@@ -117,7 +117,7 @@ def gen(horizon):
         for it in range(0, 2 * member.num_segment * 20 + 1, 20):
             member.set_iteration(20, it)
             rows.append(member.get_gait_table().copy())
-        tables[member.name] = np.array(rows)
+        tables[member._name_] = np.array(rows)   # Enum key (Gait.name is overridden, gait.py:52-54)
     np.savez_compressed(os.path.join(HERE, f"gait_N{N}.npz"), **tables)
 
     if N == 16:

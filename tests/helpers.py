@@ -14,8 +14,9 @@ def oracle_solution(batch, b, horizon):
     rec = batch["robot"][b]
     inertia = np.array([[rec[1], rec[2], rec[3]], [rec[2], rec[4], rec[5]],
                         [rec[3], rec[5], rec[6]]], dtype=np.float32)
+    normal = rec[9:12].astype(np.float64)
     o = F.formulate(x0, xref, contact, feet, inertia, float(rec[0]), horizon,
-                    mu=float(rec[7]), fz_max=float(rec[8]))
+                    mu=float(rec[7]), fz_max=float(rec[8]), normal=normal)
     x, y, info = Q.solve_qp_dual_active_set(o["H"], o["g"], o["C"], o["lb"], o["ub"])
     return x, o, info
 

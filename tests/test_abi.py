@@ -1,0 +1,72 @@
+"""CPU: the C-ABI library loads, exports every symbol include/mpcqp.h declares,
+and its host-side contract holds without a GPU (no compute calls)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "mpcqp.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:[a-zA-Z_][\w\s\*]*?)\b(mpcqp_\w+)\s*\(", src, re.M)))
+
+
+def test_header_and_binding_agree():
+    from mpcqp import _lib
+    assert _declared() == sorted(_lib.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    from mpcqp import _lib
+    lib = _lib.load()
+    for name in _declared():
+        assert hasattr(lib, name), name
+    assert lib.mpcqp_abi_version() == 1
+
+
+def test_params_struct_layout():
+    from mpcqp import _lib
+    assert ctypes.sizeof(_lib.MpcqpParams) == 4 + 4 + 8 + 13 * 8 + 12 * 8
+
+
+def test_default_params_are_the_reference_config():
+    """mpcqp_default_params == LinearMpcConfig (linear_mpc_configs.py:4-24) + dt (mpc.py:38)."""
+    from mpcqp import _lib
+    p = _lib.default_params(16)
+    assert p.horizon == 16 and p.dt == 0.05 and p.max_iter == 0
+    assert list(p.q_diag) == [5., 5., 10., 10., 10., 50., 0.01, 0.01, 0.2, 0.2, 0.2, 0.2, 0.]
+    assert list(p.r_diag) == [1e-5] * 12
+
+
+def test_create_rejects_bad_arguments_without_crashing():
+    from mpcqp import _lib
+    lib = _lib.load()
+    ctx = ctypes.c_void_p()
+    p = _lib.default_params(0)   # horizon 0 is invalid
+    assert lib.mpcqp_create(ctypes.byref(p), 0, ctypes.byref(ctx)) == -1
+    p = _lib.default_params(10)
+    # device -1 never exists: an error code, never an exception or a crash
+    assert lib.mpcqp_create(ctypes.byref(p), -1, ctypes.byref(ctx)) != 0
+    assert lib.mpcqp_solve(None, 1, None, None, None, None, None, None, None, None, None, None) == -1
+    assert lib.mpcqp_set_stance_hint(None, 3) == -1
+    assert lib.mpcqp_destroy(None) == 0
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    """No CPU fallback: a missing .so is an error, never a silent substitute."""
+    from mpcqp import _lib
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "absent.so"))
+    with pytest.raises(_lib.MpcqpError):
+        _lib.load()
+
+
+def test_engine_refuses_cpu_device():
+    torch = pytest.importorskip("torch")
+    from mpcqp import LinearMpc
+    with pytest.raises(ValueError):
+        LinearMpc(horizon=10, device="cpu")
