@@ -1,0 +1,147 @@
+"""Drop-in ``ModelPredictiveController`` backed by the MI355X engine.
+
+Same module name, class name, constructor and methods as the reference's
+``linear_mpc/mpc.py`` (ModelPredictiveController, mpc.py:22-318), so that
+``scripts/mujoco_aliengo.py`` and ``scripts/isaacgym_a1.py`` run unchanged after
+``sys.path.append('../linear_mpc'); from mpc import ModelPredictiveController``.
+
+What changes underneath: ``_solve_mpc`` (mpc.py:262-290) no longer builds the
+QP with NumPy/SciPy and solves it with Drake; it hands (x0, X_ref, gait table,
+foot positions, robot parameters) to ``mpcqp.LinearMpc`` which formulates and
+solves on the GPU (include/mpcqp.h).  Nothing here imports pydrake, qpsolvers,
+numba, pinocchio or matplotlib.
+
+Behaviour kept from the reference:
+  * dt = 0.05 regardless of the config (mpc.py:38); the horizon is
+    read from the given config (mpc.py:39);
+  * the solver string is asserted (mpc.py:264); 'drake' and 'qpsolvers' both
+    solve the two-sided Drake-branch QP (the reference's qpsolvers branch drops
+    lb), 'hip' is accepted as well;
+  * an unsuccessful solve still returns the best iterate (mpc.py:284-286 never
+    checks is_success); a warning is emitted instead of silence.
+"""
+import math
+import os
+import sys
+import warnings
+
+import numpy as np
+
+_PKG = os.environ.get("MPCQP_PATH", os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+if _PKG not in sys.path:
+    sys.path.insert(0, _PKG)
+
+from mpcqp.params import pack_robot  # noqa: E402
+from mpcqp.reference import ReferenceTrajectory  # noqa: E402
+
+
+def quat2ZYXangle(quat):
+    """utils/kinematics.py:40-49 -- (w, x, y, z) -> [roll, pitch, yaw]."""
+    q = np.asarray(quat).reshape(-1)
+    roll = math.atan2(2 * (q[0] * q[1] + q[2] * q[3]), 1 - 2 * (q[1] ** 2 + q[2] ** 2))
+    pitch = math.asin(2 * (q[0] * q[2] - q[3] * q[1]))
+    yaw = math.atan2(2 * (q[0] * q[3] + q[1] * q[2]), 1 - 2 * (q[2] ** 2 + q[3] ** 2))
+    return [roll, pitch, yaw]
+
+
+class ModelPredictiveController():
+
+    def __init__(self, mpc_config, robot_config):
+        self.num_state = 13      # mpc.py:26
+        self.num_input = 12      # mpc.py:28
+        self.is_initialized = False
+        self.is_first_run = True
+        self._load_parameters(mpc_config, robot_config)
+        self._engine = None
+
+    def _load_parameters(self, mpc_config, robot_config):
+        """mpc.py:35-52 (Qbar/Rbar become the engine's diagonal weights)."""
+        self.dt_control = mpc_config.dt_control
+        self.iterations_between_mpc = mpc_config.iteration_between_mpc
+        self.dt = 0.05
+        self.horizon = mpc_config.horizon
+        self.mu = mpc_config.friction_coef
+        self.fz_max = robot_config.fz_max
+        self.gravity = mpc_config.gravity
+        self.base_inertia_base = robot_config.base_inertia_base
+        self.mass = robot_config.mass_base
+        self.com_height_des = robot_config.base_height_des
+        self.q_diag = np.diag(np.asarray(mpc_config.Q, dtype=np.float64)).copy()
+        self.r_diag = np.diag(np.asarray(mpc_config.R, dtype=np.float64)).copy()
+        I = np.asarray(self.base_inertia_base, dtype=np.float32)
+        self._robot_record = pack_robot(
+            dict(mass=float(self.mass), fz_max=float(self.fz_max), mu=float(self.mu),
+                 inertia=np.array([I[0, 0], I[0, 1], I[0, 2], I[1, 1], I[1, 2], I[2, 2]],
+                                  dtype=np.float32)))
+        self._ref = ReferenceTrajectory(self.horizon, self.com_height_des, batch=1, dt=self.dt,
+                                        dt_control=self.dt_control, gravity=self.gravity)
+
+    def _get_engine(self):
+        if self._engine is None:
+            from mpcqp import LinearMpc
+            self._engine = LinearMpc(horizon=self.horizon, robot=self._robot_record, dt=self.dt,
+                                     Q=self.q_diag, R=self.r_diag,
+                                     device=os.environ.get("MPCQP_DEVICE", "cuda:0"))
+        return self._engine
+
+    # data: [pos_base, vel_base, quat_base, omega_base, ...]   (mpc.py:54-79)
+    def update_robot_state(self, robot_data):
+        if not self.is_initialized:
+            self.current_state = np.zeros(13, dtype=np.float32)
+            self.roll_init = 0.0
+            self.pitch_init = 0.0
+            self.is_initialized = True
+        self.__robot_data = robot_data
+        rpy_base = quat2ZYXangle(robot_data.quat_base)
+        pos_base = np.array(robot_data.pos_base, dtype=np.float32)
+        omega_base = np.array(robot_data.ang_vel_base, dtype=np.float32)
+        vel_base = np.array(robot_data.lin_vel_base, dtype=np.float32)
+        self.current_state[0:3] = rpy_base
+        self.current_state[3:6] = pos_base
+        self.current_state[6:9] = omega_base
+        self.current_state[9:12] = vel_base
+        self.current_state[12] = -self.gravity          # mpc.py:76
+        self.yaw = rpy_base[2]
+        self.pos_base_feet = robot_data.pos_base_feet   # world frame, relative to the CoM
+
+    def update_mpc_if_needed(self, iter_counter, base_vel_base_des, yaw_turn_rate_des,
+                             gait_table, solver='drake', debug=False, iter_debug=None):
+        """mpc.py:81-108."""
+        vel_base_des = self.__robot_data.R_base @ base_vel_base_des
+        self._ref.integrate_desired(self.yaw, vel_base_des, yaw_turn_rate_des)
+        self.xpos_base_desired = float(self._ref.xpos_des[0])
+        self.ypos_base_desired = float(self._ref.ypos_des[0])
+        self.yaw_desired = float(self._ref.yaw_des[0])
+        self.is_first_run = False
+        if iter_counter % self.iterations_between_mpc == 0:
+            ref_traj = self.generate_reference_trajectory(vel_base_des, yaw_turn_rate_des)
+            self.ref_traj = ref_traj
+            self.__contact_forces = self._solve_mpc(ref_traj, gait_table, solver=solver)[0:12]
+            if debug and iter_counter == iter_debug:
+                warnings.warn("debug CoM-trajectory plot (mpc.py:293-318) is not provided by the engine")
+        return self.__contact_forces[0:12]
+
+    def generate_reference_trajectory(self, vel_base_des, yaw_turn_rate):
+        """mpc.py:110-170 (stateful clamp + roll/pitch compensation)."""
+        X = self._ref.trajectory(self.current_state[None, :], np.asarray(vel_base_des)[None, :],
+                                 yaw_turn_rate)[0]
+        self.xpos_base_desired = float(self._ref.xpos_des[0])
+        self.ypos_base_desired = float(self._ref.ypos_des[0])
+        self.roll_init = float(self._ref.roll_init[0])
+        self.pitch_init = float(self._ref.pitch_init[0])
+        return X
+
+    def _solve_mpc(self, ref_traj, gait_table, solver='drake', debug=False):
+        """mpc.py:262-290 -> one engine call; returns U[12N] (float64, like Drake)."""
+        assert solver == 'drake' or solver == 'qpsolvers' or solver == 'hip'
+        feet = np.asarray([np.asarray(f, dtype=np.float64).reshape(3) for f in self.pos_base_feet],
+                          dtype=np.float32)
+        res = self._get_engine().solve(self.current_state[None, :],
+                                       np.asarray(ref_traj, dtype=np.float32)[None, :],
+                                       np.asarray(gait_table, dtype=np.float32)[None, :],
+                                       feet[None, :, :], return_all=True)
+        U = res.U.cpu().numpy().reshape(-1).astype(np.float64)
+        status = int(res.status.cpu().numpy()[0])
+        if status != 0:
+            warnings.warn(f"mpcqp: robot solve status {status}; returning the best iterate")
+        return U

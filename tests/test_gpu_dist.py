@@ -1,0 +1,24 @@
+"""GPU: bench.py's single-GPU path end to end (one JSON line, the contract fields)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.gpu
+
+
+def test_bench_contract_line():
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
+                          "--cpu-seconds", "0.5"], capture_output=True, text=True, timeout=600, check=True)
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in line, k
+    assert line["value"] > 0 and line["n_gpus"] == 1 and line["scaling"] == "weak"
+    assert set(line["roofline"]) == {"bound", "achieved", "peak", "unit", "frac", "traffic"}
+    assert line["cpu_baseline"]["kind"] == "port" and line["cpu_baseline"]["cores"] == 1
+    assert line["status_ok_frac"] == 1.0
