@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--no-gather", action="store_true", help="skip the end-of-step u0 gather")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "latest", "pmc_traffic.json"))
     return ap.parse_args()
 
 

@@ -1,0 +1,83 @@
+"""Summarise a tools/profile.sh run into profiles/<tag>/.
+
+Copies the kernel-trace stats CSV and derives, for the engine kernel, the
+average dispatch duration and HBM traffic per launch from the PMC passes:
+  FETCH_SIZE, WRITE_SIZE are in KiB per dispatch (rocprofv3, gfx950).
+  MI355X_MICROARCH.md §HBM: FETCH_SIZE reads exactly 1/2 of the bytes of a wide
+  (16 B/lane) coalesced stream; other widths are uncalibrated.  The engine's
+  loads are 4-B-per-lane staging loads, so both the raw and the x2-corrected
+  read figures are reported.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+KERNEL = "mpcqp"
+
+
+def rows(pattern):
+    out = []
+    for f in glob.glob(pattern, recursive=True):
+        with open(f) as fh:
+            out.extend(csv.DictReader(fh))
+    return out
+
+
+def counter(run_dir, name):
+    vals = []
+    for r in rows(os.path.join(run_dir, "**", "*counter_collection.csv")):
+        if KERNEL in r.get("Kernel_Name", "") and r.get("Counter_Name") == name:
+            vals.append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    args = sys.argv[3:]
+    os.makedirs(dst, exist_ok=True)
+    for f in glob.glob(os.path.join(src, "kt", "**", "*stats.csv"), recursive=True):
+        shutil.copy(f, os.path.join(dst, os.path.basename(f)))
+    stats = rows(os.path.join(src, "kt", "**", "*kernel_stats.csv"))
+    eng = [r for r in stats if KERNEL in r["Name"]]
+    avg_ns = float(eng[0]["AverageNs"]) if eng else None
+    fetch = counter(os.path.join(src, "fetch"), "FETCH_SIZE")
+    write = counter(os.path.join(src, "write"), "WRITE_SIZE")
+    bench = {}
+    try:
+        with open(os.path.join(src, "bench_kt.json")) as fh:
+            bench = json.loads(fh.read().strip().splitlines()[-1])
+    except Exception:
+        pass
+    cfg = "config2"
+    for i, a in enumerate(args):
+        if a == "--config" and i + 1 < len(args):
+            cfg = args[i + 1]
+    batch = bench.get("config", {}).get("batch_per_gpu")
+    fk = sum(fetch) / len(fetch) if fetch else None
+    wk = sum(write) / len(write) if write else None
+    entry = {
+        "batch": batch,
+        "kernel_avg_ns_rocprof": avg_ns,
+        "kernel_ms_avg_bench_events": bench.get("kernel_ms_avg"),
+        "fetch_kib_per_launch_raw": fk,
+        "write_kib_per_launch": wk,
+        "hbm_bytes_per_launch": (2 * fk * 1024 + wk * 1024) if fk is not None and wk is not None else None,
+        "hbm_bytes_per_launch_uncorrected": (fk * 1024 + wk * 1024) if fk is not None and wk is not None else None,
+        "note": "FETCH_SIZE x2 per MI355X_MICROARCH.md (wide-stream calibration; 4-B staging loads are uncalibrated)",
+    }
+    path = os.path.join(dst, "pmc_traffic.json")
+    data = {}
+    if os.path.exists(path):
+        with open(path) as fh:
+            data = json.load(fh)
+    data[cfg] = entry
+    with open(path, "w") as fh:
+        json.dump(data, fh, indent=2)
+    print(json.dumps({cfg: entry}))
+
+
+if __name__ == "__main__":
+    main()
