@@ -65,7 +65,8 @@ constexpr int SCR = LANES * LDM;                                     // 4224 dou
 constexpr int IN_X0 = 0, IN_FEET = 13, IN_ROBOT = 25, IN_CONTACT = 44, IN_XREF = 44 + 4 * kMaxN;
 constexpr int IN_END = IN_XREF + NX * kMaxN;
 static_assert(SCR0 * 2 + IN_END <= SCR * 2, "staged inputs do not fit");
-constexpr int PV = LANES + 4;           // padded broadcast vector: element i at pv(i)
+constexpr int PV = LANES + 4;
+constexpr int NL_CAP = 126;             // variables of the large class (mpcqp_large.h)           // padded broadcast vector: element i at pv(i)
 
 // i -> i + 2*(i/32): the 8 column segments {8tc..8tc+7} land on distinct bank groups
 __host__ __device__ constexpr int pv(int i) { return i + 2 * (i >> 5); }
@@ -334,7 +335,8 @@ __device__ __forceinline__ void write_empty(int b, int lane, int N, int code, fl
 __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(1, 2))) void mpcqp_kernel(
     KParams P, int B, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
-    float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg) {
+    float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
+    int* __restrict__ queue) {
   __shared__ Shared sm;
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
@@ -400,6 +402,10 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(1, 2))) v
   }
   const int n = 3 * S, m = 6 * S;
   if (n > NV) {
+    if (queue && n <= NL_CAP) {   // the 8-wave class (mpcqp_kernel_large) takes it
+      if (lane == 0) queue[4 + atomicAdd(&queue[0], 1)] = b;
+      return;
+    }
     write_empty(b, lane, N, MPCQP_STATUS_TOO_LARGE, u0g, Ug, statusg, itersg);
     return;
   }
@@ -857,6 +863,9 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(1, 2))) v
   }
 }
 
+#include "mpcqp_large.h"
+static_assert(NL - 2 == NL_CAP, "large-class capacity");
+
 }  // namespace
 
 // ============================================================== C ABI
@@ -864,6 +873,9 @@ struct mpcqp_ctx {
   mpcqp_params params;
   int device;
   int stance_hint;
+  int ncu;
+  int qcap;           // robots the device queue can hold
+  int* queue;         // [count, next, exited, pad, robots...] for the large class
   std::string err;
 };
 
@@ -899,6 +911,12 @@ int mpcqp_create(const mpcqp_params* p, int32_t device, mpcqp_ctx** out) {
   ctx->params = *p;
   ctx->device = device;
   ctx->stance_hint = 0;
+  ctx->queue = nullptr;
+  ctx->qcap = 0;
+  ctx->ncu = 0;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->ncu = prop.multiProcessorCount;
+  if (ctx->ncu <= 0) ctx->ncu = 256;
   *out = ctx;
   return MPCQP_OK;
 }
@@ -925,14 +943,35 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   for (int i = 0; i < NX; ++i) kp.q[i] = ctx->params.q_diag[i];
   for (int i = 0; i < NU; ++i) kp.r[i] = ctx->params.r_diag[i];
   hipStream_t st = (hipStream_t)stream;
+  // robots with more than 64 stance variables are queued for the 8-wave class,
+  // unless the caller promised (stance hint) that none exceeds one wave
+  const bool large = !(ctx->stance_hint > 0 && 3 * ctx->stance_hint <= NV);
+  if (large && batch > ctx->qcap) {
+    if (ctx->queue) (void)hipFree(ctx->queue);
+    ctx->queue = nullptr;
+    ctx->qcap = 0;
+    if (hipMalloc(&ctx->queue, sizeof(int) * (4 + (size_t)batch)) != hipSuccess)
+      return set_err(ctx, MPCQP_ERR_ALLOC, "queue allocation failed");
+    if (hipMemset(ctx->queue, 0, sizeof(int) * 4) != hipSuccess)
+      return set_err(ctx, MPCQP_ERR_HIP, "queue init failed");
+    ctx->qcap = batch;
+  }
+  int* q = large ? ctx->queue : nullptr;
   hipLaunchKernelGGL(mpcqp_kernel, dim3(batch), dim3(LANES), 0, st, kp, (int)batch, x0, xref, contact, feet,
-                     robot, u0, U, (int*)status, (int*)iters);
+                     robot, u0, U, (int*)status, (int*)iters, q);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch: ") + hipGetErrorString(e));
+  if (large) {
+    hipLaunchKernelGGL(mpcqp_kernel_large, dim3(batch), dim3(LT), 0, st, kp, x0, xref, contact, feet, robot, u0, U,
+                       (int*)status, (int*)iters, q);
+    e = hipGetLastError();
+    if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (large): ") + hipGetErrorString(e));
+  }
   return MPCQP_OK;
 }
 
 int mpcqp_destroy(mpcqp_ctx* ctx) {
+  if (ctx && ctx->queue) (void)hipFree(ctx->queue);
   delete ctx;
   return MPCQP_OK;
 }

@@ -22,12 +22,13 @@ PHASES = ["inputs+model+discretise", "g,Y,T", "H rows", "sweep H^-1", "active se
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
     N = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    gaits = tuple(sys.argv[3].split(",")) if len(sys.argv) > 3 else ("trot10",)
     _lib.LIB_PATH = os.path.join(ROOT, "pympc-quadruped_amd", "mpcqp", "libmpcqp_stamps.so")
     lib = _lib.load()
     p = _lib.default_params(N)
     ctx = ctypes.c_void_p()
     _lib.check(None, lib.mpcqp_create(ctypes.byref(p), 0, ctypes.byref(ctx)), "create")
-    bt = make_batch(B, N, seed=1000, gaits=("trot10",), robots=("a1",))
+    bt = make_batch(B, N, seed=1000, gaits=gaits, robots=("a1",))
     dev = torch.device("cuda:0")
     d = {k: torch.as_tensor(v).to(dev).contiguous() for k, v in bt.items()}
     u0 = torch.empty((B, 12), device=dev)
