@@ -93,6 +93,7 @@ struct alignas(16) Shared {
   double rows[6][3];    // cone rows a_r, shared by every foot of the robot
   double ii[9];         // inverse world inertia (float32-rounded)
   double x0[NX], y1[NX], y2[NX];
+  double qd[NX], rd[NU];   // cost weights (kernel arguments indexed at run time would be memory loads)
   double ub[SMAX + 1];
   int foot_t[SMAX + 1], foot_leg[SMAX + 1];
   int stance_of[4 * kMaxN];
@@ -234,15 +235,16 @@ __device__ __forceinline__ double tile_matvec(const double (&W)[8][8], const dou
   return keep + dpp_d<DPP_XOR1>(send);
 }
 
-// One pivot of the symmetric sweep; K compile-time so W stays in VGPRs.
+// One pivot K = 8 KT + KC of the symmetric sweep; KC compile-time so W stays in
+// VGPRs, KT a runtime loop index so the code (8 pivots) stays in the I-cache.
 // W_ij -= z_i z_j / d (i,j != K), W_iK = z_i/d, W_KK = -1/d; the pivot row uses
 // W_Kj = z_j (symmetry): W_Kj + (1/d - 1) z_j = z_j/d.  Ends at -H^-1.
 // Rows/columns >= n are identity padding: z = 0 there, they never change.
-template <int K>
-__device__ __forceinline__ void sweep_step(double (&W)[8][8], Shared& sm, int tr, int tc, int n) {
+template <int KC>
+__device__ __forceinline__ void sweep_pivot(double (&W)[8][8], Shared& sm, int tr, int tc, int KT, int n) {
+  const int K = 8 * KT + KC;
   if (K < n) {   // wave-uniform
-    constexpr int KT = K >> 3, KC = K & 7;
-    double* const zc = sm.zc[K & 1];
+    double* const zc = sm.zc[KC & 1];
     if (tc == KT) {
       double col[8];
 #pragma unroll
@@ -272,10 +274,11 @@ __device__ __forceinline__ void sweep_step(double (&W)[8][8], Shared& sm, int tr
   }
 }
 
-template <int... Ks>
-__device__ __forceinline__ void sweep_all(double (&W)[8][8], Shared& sm, int tr, int tc, int n,
-                                          std::integer_sequence<int, Ks...>) {
-  (sweep_step<Ks>(W, sm, tr, tc, n), ...);
+__device__ __forceinline__ void sweep_all(double (&W)[8][8], Shared& sm, int tr, int tc, int n) {
+#pragma unroll 1
+  for (int KT = 0; 8 * KT < n; ++KT) {
+    static_for<8>([&](auto C) { sweep_pivot<decltype(C)::value>(W, sm, tr, tc, KT, n); });
+  }
 }
 
 // y_lane = sum_{k < 8*nch} M[lane][k] vec[k]   (row of M in LDS, vec broadcast), b128 loads
@@ -417,6 +420,8 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(1, 2))) v
   double* const X = scr + OFF_X;   // X_p[s][c] at X + p*NX*NU + s*NU + c
   for (int k = lane; k < NX * NX + NX * NU; k += LANES) (k < NX * NX ? Ac[k] : Bc[k - NX * NX]) = 0.0;
   if (lane < NX) sm.x0[lane] = (double)in[IN_X0 + lane];
+  if (lane < NX) sm.qd[lane] = P.q[lane];
+  if (lane < NU) sm.rd[lane] = P.r[lane];
 
   // ------------------------------------------------ 1. model (mpc.py:173-192)
   // Reference dtypes: Rz float32 of float64 cos/sin; I_w = Rz I Rz^T float32;
@@ -586,7 +591,7 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(1, 2))) v
           const int ja = 16 * I + li, jb = 16 * J + li;
           double a = 0.0, bq = 0.0;
           if (s < NX && ja < NY) a = X[(ja / NU) * NX * NU + s * NU + ja % NU];
-          if (s < NX && jb < NY) bq = P.q[s] * X[(jb / NU) * NX * NU + s * NU + jb % NU];
+          if (s < NX && jb < NY) bq = sm.qd[s] * X[(jb / NU) * NX * NU + s * NU + jb % NU];
           acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bq, acc, 0, 0, 0);
         }
 #pragma unroll
@@ -616,6 +621,8 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(1, 2))) v
   // H tile (rows 8tr.., cols 8tc..) into registers; rows/cols >= n are identity padding
   double W[8][8];
   {
+    // one runtime loop over the tile rows (compact code: the H build runs once per
+    // robot, so its instructions would otherwise stream through the I-cache once)
     int cj[8], cc[8];
     static_for<8>([&](auto C) {
       constexpr int c = decltype(C)::value;
@@ -624,14 +631,19 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(1, 2))) v
       cj[c] = sm.foot_t[sb];
       cc[c] = 3 * sm.foot_leg[sb] + col % 3;
     });
-    static_for<8>([&](auto R) {
-      constexpr int r = decltype(R)::value;
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) W[r][c] = 0.0;
+#pragma unroll 1
+    for (int r = 0; r < 8; ++r) {
       const int row = 8 * tr + r;
       const bool rowv = row < n;
       const int sa = rowv ? row / 3 : 0;
       const int ja = sm.foot_t[sa];
       const int ca = 3 * sm.foot_leg[sa] + row % 3;
-      const double r2 = 2.0 * P.r[rowv ? ca : 0];
+      const double r2 = 2.0 * sm.rd[rowv ? ca : 0];
+      double h[8];
       static_for<8>([&](auto Cc) {
         constexpr int c = decltype(Cc)::value;
         const int col = 8 * tc + c;
@@ -643,16 +655,20 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(1, 2))) v
           const int p = pq / 3, q = pq % 3;
           acc = fma(T[(le ? pq : q * 3 + p) * nT + ti], Y[pq * NU * NU + ca * NU + cc[c]], acc);
         }
-        const double h = 2.0 * acc + (row == col ? r2 : 0.0);
-        W[r][c] = (rowv && col < n) ? h : (row == col ? 1.0 : 0.0);
+        const double hv = 2.0 * acc + (row == col ? r2 : 0.0);
+        h[c] = (rowv && col < n) ? hv : (row == col ? 1.0 : 0.0);
       });
-      MPCQP_FENCE();   // one row at a time: bounds the VGPRs held by in-flight loads
-    });
+      static_for<8>([&](auto Rr) {
+        constexpr int rr = decltype(Rr)::value;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) W[rr][c] = (rr == r) ? h[c] : W[rr][c];
+      });
+    }
   }
   STAMP(3);
 
   // ------------------------------------------------ 4. W = H^-1 (symmetric sweep)
-  sweep_all(W, sm, tr, tc, n, std::make_integer_sequence<int, NV>{});
+  sweep_all(W, sm, tr, tc, n);
 #pragma unroll
   for (int r = 0; r < 8; ++r)
 #pragma unroll

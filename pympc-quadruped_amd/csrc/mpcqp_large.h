@@ -24,6 +24,7 @@ constexpr int PL = NL + 8;             // padded vector (pv(127) = 133)
 constexpr int DPP_ROR8 = 0x128;        // row_ror:8 -> lane i <-> i ^ 8 inside 16 lanes
 
 struct alignas(16) LShared {
+  static_assert(PL % 2 == 0, "16-B vector rows");
   // formulation
   double Ac[NX * NX], Nm[NX * NX], Bc[NX * NU];
   double X[3 * NX * NU];               // X_p[s][c]
@@ -32,15 +33,20 @@ struct alignas(16) LShared {
   double Y[9 * NU * NU];               // Y_pq[c][c2]
   double T[9 * kNT];                   // Toeplitz weights
   double x0[NX], y1[NX], y2[NX];
+  double qd[NX], rd[NU];               // cost weights
   double ii[9];
   double rows[6][3];
   double ub[SL + 1];
-  // solve
-  double vb[PL];                       // matvec right-hand side (padded)
-  double zc[2][PL];                    // sweep pivot column, double-buffered
-  double rr[PL];                       // r = Minv mp (padded, slot-indexed)
-  double cv[PL];                       // dropped column of Minv (padded)
-  double wv[NL], zv[NL], rv[PL], gv[NL];
+  // solve -- every vector read with ds_read_b128 is 16-B aligned (an unaligned
+  // b128 access is replayed at ~64 cycles per wave-instruction)
+  alignas(16) double vb[PL];           // matvec right-hand side (padded)
+  alignas(16) double zc[2][PL];        // sweep pivot column, double-buffered
+  alignas(16) double rr[PL];           // r = Minv mp (padded, slot-indexed)
+  alignas(16) double cv[PL];           // dropped column of Minv (padded)
+  alignas(16) double rv[PL];
+  alignas(16) double wv[NL];
+  alignas(16) double zv[NL];
+  alignas(16) double gv[NL];
   double redv[2][LW];                  // per-wave argmin partials (double-buffered)
   int redi[2][LW];
   double bc_zs, bc_s;                  // zs_p, s_p broadcast
@@ -124,12 +130,16 @@ __device__ __forceinline__ int lwg_argmin(double v, int idx, LShared& sm, int wa
   return uni(bi);
 }
 
-// One pivot of the symmetric sweep over the 4x8 tiles (see sweep_step).
-template <int K>
-__device__ __forceinline__ void lsweep_step(double (&W)[4][8], LShared& sm, int tr, int tc, int n) {
+// One pivot K = 8 KT + KC of the symmetric sweep over the 4x8 tiles (see
+// sweep_step).  KC is compile-time (register column), KT a runtime loop index:
+// the sweep's code is 8 pivots long, so it stays in the instruction cache.
+template <int KC>
+__device__ __forceinline__ void lsweep_pivot(double (&W)[4][8], LShared& sm, int tr, int tc, int KT, int n) {
+  const int K = 8 * KT + KC;
   if (K < n) {
-    constexpr int KT = K >> 3, KC = K & 7, KR = K >> 2, KRR = K & 3;
-    double* const zc = sm.zc[K & 1];
+    constexpr int KRR = KC & 3;
+    const int KR = 2 * KT + (KC >> 2);
+    double* const zc = sm.zc[KC & 1];
     if (tc == KT) {
       d2* p = reinterpret_cast<d2*>(zc + pv(4 * tr));
       p[0] = d2{W[0][KC], W[1][KC]};
@@ -158,10 +168,15 @@ __device__ __forceinline__ void lsweep_step(double (&W)[4][8], LShared& sm, int 
   }
 }
 
-template <int... Ks>
 __device__ __forceinline__ void lsweep_all(double (&W)[4][8], LShared& sm, int tr, int tc, int n,
-                                           std::integer_sequence<int, Ks...>) {
-  (lsweep_step<Ks>(W, sm, tr, tc, n), ...);
+                                           unsigned long long* dbg) {
+#pragma unroll 1
+  for (int KT = 0; 8 * KT < n; ++KT) {
+#ifdef MPCQP_STAMPS
+    if (dbg && threadIdx.x == 0) dbg[KT] = __builtin_amdgcn_s_memtime();
+#endif
+    static_for<8>([&](auto C) { lsweep_pivot<decltype(C)::value>(W, sm, tr, tc, KT, n); });
+  }
 }
 
 __device__ __forceinline__ void lwrite_empty(int b, int tid, int N, int code, float* u0g, float* Ug, int* statusg,
@@ -254,6 +269,8 @@ __device__ __forceinline__ void lsolve_robot(const KParams& P, int b, LShared& s
   double* const Bc = sm.Bc;
   for (int k = tid; k < NX * NX + NX * NU; k += LT) (k < NX * NX ? Ac[k] : Bc[k - NX * NX]) = 0.0;
   if (tid < NX) sm.x0[tid] = (double)in[IN_X0 + tid];
+  if (tid < NX) sm.qd[tid] = P.q[tid];
+  if (tid < NU) sm.rd[tid] = P.r[tid];
   {
     const double yaw = (double)in[IN_X0 + 2];
     const double c = f32r(cos(yaw)), s = f32r(sin(yaw));
@@ -391,7 +408,7 @@ __device__ __forceinline__ void lsolve_robot(const KParams& P, int b, LShared& s
       const int ja = 16 * I + li, jb = 16 * J + li;
       double a = 0.0, bq = 0.0;
       if (s < NX && ja < NY) a = X[(ja / NU) * NX * NU + s * NU + ja % NU];
-      if (s < NX && jb < NY) bq = P.q[s] * X[(jb / NU) * NX * NU + s * NU + jb % NU];
+      if (s < NX && jb < NY) bq = sm.qd[s] * X[(jb / NU) * NX * NU + s * NU + jb % NU];
       acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bq, acc, 0, 0, 0);
     }
 #pragma unroll
@@ -435,6 +452,8 @@ __device__ __forceinline__ void lsolve_robot(const KParams& P, int b, LShared& s
   // H tile (rows 4tr.., cols 8tc..) into registers; identity padding beyond n
   double W[4][8];
   {
+    // one runtime loop over the tile rows (compact code: the H build runs once per
+    // robot, so its instructions would otherwise stream through the I-cache once)
     int cj[8], cc[8];
     static_for<8>([&](auto C) {
       constexpr int c = decltype(C)::value;
@@ -443,14 +462,19 @@ __device__ __forceinline__ void lsolve_robot(const KParams& P, int b, LShared& s
       cj[c] = sm.foot_t[sb];
       cc[c] = 3 * sm.foot_leg[sb] + col % 3;
     });
-    static_for<4>([&](auto R) {
-      constexpr int r = decltype(R)::value;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) W[r][c] = 0.0;
+#pragma unroll 1
+    for (int r = 0; r < 4; ++r) {
       const int row = 4 * tr + r;
       const bool rowv = row < n;
       const int sa = rowv ? row / 3 : 0;
       const int ja = sm.foot_t[sa];
       const int ca = 3 * sm.foot_leg[sa] + row % 3;
-      const double r2 = 2.0 * P.r[rowv ? ca : 0];
+      const double r2 = 2.0 * sm.rd[rowv ? ca : 0];
+      double h[8];
       static_for<8>([&](auto Cc) {
         constexpr int c = decltype(Cc)::value;
         const int col = 8 * tc + c;
@@ -462,16 +486,20 @@ __device__ __forceinline__ void lsolve_robot(const KParams& P, int b, LShared& s
           const int p = pq / 3, q = pq % 3;
           acc = fma(sm.T[(le ? pq : q * 3 + p) * nT + ti], sm.Y[pq * NU * NU + ca * NU + cc[c]], acc);
         }
-        const double h = 2.0 * acc + (row == col ? r2 : 0.0);
-        W[r][c] = (rowv && col < n) ? h : (row == col ? 1.0 : 0.0);
+        const double hv = 2.0 * acc + (row == col ? r2 : 0.0);
+        h[c] = (rowv && col < n) ? hv : (row == col ? 1.0 : 0.0);
       });
-      MPCQP_FENCE();
-    });
+      static_for<4>([&](auto Rr) {
+        constexpr int rr = decltype(Rr)::value;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) W[rr][c] = (rr == r) ? h[c] : W[rr][c];
+      });
+    }
   }
 
   STAMP(3);
   // ------------------------------------------------ 4. W = H^-1 (symmetric sweep)
-  lsweep_all(W, sm, tr, tc, n, std::make_integer_sequence<int, NL - 2>{});
+  lsweep_all(W, sm, tr, tc, n, Ug ? (unsigned long long*)(Ug + (size_t)b * N * 12) + 8 : nullptr);
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll

@@ -113,6 +113,39 @@ __global__ void lds_b128_bcast(double* out, int iters, unsigned long long* cyc) 
   if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+// LDS write -> workgroup barrier -> LDS read of another wave's value, per iteration
+__global__ void bar_lds(double* out, int iters, unsigned long long* cyc) {
+  __shared__ double buf[1024];
+  const int t = threadIdx.x, nt = blockDim.x;
+  double v = t;
+  unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < iters; ++it) {
+    buf[(it & 1) * 512 + t] = v;
+    __syncthreads();
+    v += buf[(it & 1) * 512 + (t + 64) % nt] * 1e-9;
+  }
+  unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  out[t] = v;
+  if (t == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+// 32 independent f64 FMAs per iteration with a barrier every iteration
+__global__ void bar_fma(double* out, int iters, unsigned long long* cyc) {
+  double a[32];
+  for (int i = 0; i < 32; ++i) a[i] = threadIdx.x * 1e-3 + i;
+  const double b = 1.0000001, c = 1e-9;
+  unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int i = 0; i < 32; ++i) a[i] = fma(a[i], b, c);
+    __syncthreads();
+  }
+  unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  double s = 0; for (int i = 0; i < 32; ++i) s += a[i];
+  out[threadIdx.x] = s;
+  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
 int main() {
   double* d; float* f; unsigned long long* c;
   hipMalloc(&d, 1 << 20); hipMalloc(&f, 1 << 20); hipMalloc(&c, 1 << 16);
@@ -135,6 +168,18 @@ int main() {
   run("mfma_f64_16x16x4 (4 acc)", mfma_f64, 1024, 4);
   run("16x ds_read_b128 bcast", lds_b128_bcast, 1, 16);
   run("16x ds_read bcast+wait", lds_b128_burst, 1, 1);
+  for (int nt = 64; nt <= 512; nt *= 2) {
+    for (int g : {1, 256}) {
+      hipLaunchKernelGGL(bar_lds, dim3(g), dim3(nt), 0, 0, d, 2000, c);
+      hipLaunchKernelGGL(bar_lds, dim3(g), dim3(nt), 0, 0, d, 2000, c);
+      hipDeviceSynchronize(); hipMemcpy(h, c, 8, hipMemcpyDeviceToHost);
+      printf("write+barrier+read   %3d thr grid %3d: %.1f cycles/iter\n", nt, g, (double)h[0] / 2000);
+      hipLaunchKernelGGL(bar_fma, dim3(g), dim3(nt), 0, 0, d, 2000, c);
+      hipLaunchKernelGGL(bar_fma, dim3(g), dim3(nt), 0, 0, d, 2000, c);
+      hipDeviceSynchronize(); hipMemcpy(h, c, 8, hipMemcpyDeviceToHost);
+      printf("32 fma_f64 + barrier %3d thr grid %3d: %.1f cycles/iter\n", nt, g, (double)h[0] / 2000);
+    }
+  }
   hipLaunchKernelGGL(memtime_vs_realtime, dim3(1), dim3(64), 0, 0, c);
   hipDeviceSynchronize(); hipMemcpy(h, c, 16, hipMemcpyDeviceToHost);
   printf("s_memtime ticks %llu vs realtime(100MHz) %llu -> %.3f GHz\n", h[0], h[1], h[0] / (h[1] / 100e6) / 1e9);
