@@ -1,0 +1,589 @@
+// mpcqp_solve.h -- one robot's formulate + solve by one workgroup (included by
+// mpcqp.hip inside its anonymous namespace).
+//
+// Capacity class NV (stance variables n = 3 * #stance <= NV):
+//   NV =  64: 2 waves (128 threads) per robot -- every trot/pace/bound schedule at N <= 10
+//   NV = 128: 8 waves (512 threads) per robot -- N = 16/20 schedules, standing at N <= 10
+// Register tiles: lane t = (tr, tc) = (t / TCN, t % TCN) holds rows 4tr..4tr+3 and
+// columns 8tc..8tc+7 of each NV x NV matrix (32 doubles per matrix per lane).
+//
+// Solver: Goldfarb-Idnani dual active set (Math. Prog. 27, 1983) on
+//   min 1/2 x^T H x + g^T x   s.t.  a_c . x >= b_c  (6 one-sided cone rows per foot-step)
+// in "projected" form.  With W = H^-1 and the active rows A:
+//   P = W - (A W)^T (A W A^T)^-1 (A W)     (n x n, reduced inverse Hessian)
+//   R = (A W A^T)^-1 A W                   (slots x n)
+// the primal / dual step directions for a violated row p are z = P a_p and
+// r = R a_p; a_p touches the 3 variables of one foot-step, so both are
+// combinations of 3 register columns (no matrix-vector product per iteration).
+// Adding p into free slot q:   P -= z z^T / s,   R -= (r - e_q) z^T / s   (s = a_p . z)
+// Dropping slot l (eta = Minv_ll, y = Minv[:, l] = R H R_l^T):
+//                              P += R_l^T R_l / eta,   R -= y R_l / eta,  R_l = 0.
+// Scalar state (constraint values s, x, multipliers u, the active-slot mask) is
+// kept redundantly by every wave, so one iteration needs ONE workgroup barrier
+// (the z / r exchange) and every wave reaches the same decisions.
+
+template <int NV>
+struct Cfg {
+  static constexpr int NW = NV * NV / 2048;   // waves per robot
+  static constexpr int NT = NW * LANES;
+  static constexpr int TCN = NV / 8;          // tile columns (lanes per tile row)
+  static constexpr int RPW = 256 / TCN;       // tile rows (slots / variables) per wave
+  static constexpr int CPL = NV / 32;         // constraint rows per lane (m = 6S <= 2NV)
+  static constexpr int VPL = NV / 64;         // variables / slots per lane
+  static_assert(NW * LANES * 32 == NV * NV, "4 x 8 tiles");
+};
+
+template <int NV>
+struct alignas(16) SharedT {
+  Form f;
+  RobotMeta mt;
+  alignas(16) double zc[2][NV];   // sweep pivot column (double-buffered)
+  alignas(16) double vz[2][NV];   // z = P a_p (double-buffered by iteration)
+  alignas(16) double vr[2][NV];   // r = R a_p (slot-indexed)
+  alignas(16) double vx[NV];      // x
+  alignas(16) double gv[NV];      // g
+  alignas(16) double rl[NV];      // drop path: R_l, H R_l^T, R H R_l^T
+  alignas(16) double tv[NV];
+  alignas(16) double yv[NV];
+  double wmax[Cfg<NV>::NW];
+};
+
+constexpr int DPP_SHL1 = 0x101;   // row_shl:1 -- lane i reads lane i + 1 (same 16-lane row)
+constexpr int DPP_ROR8 = 0x128;   // row_ror:8 -- lane i <-> i ^ 8 inside 16 lanes
+
+__device__ __forceinline__ double dpp_shl1(double v) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)bits, DPP_SHL1, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(bits >> 32), DPP_SHL1, 0xF, 0xF, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Sum 4 row partials over the TCN lanes of a tile row.  Lane keeps row
+// 4tr + 2 bit2(lane) + bit1(lane) (see trow / twriter).
+template <int TCN>
+__device__ __forceinline__ double tile_reduce(const double (&acc)[4], int lane) {
+  const bool hi4 = (lane & 4) != 0;
+  double k2[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const double send = hi4 ? acc[k] : acc[2 + k];
+    const double keep = hi4 ? acc[2 + k] : acc[k];
+    k2[k] = keep + dpp_d<DPP_HMIRROR>(send);
+  }
+  const bool hi2 = (lane & 2) != 0;
+  const double send = hi2 ? k2[0] : k2[1];
+  const double keep = hi2 ? k2[1] : k2[0];
+  double y = keep + dpp_d<DPP_XOR2>(send);
+  y += dpp_d<DPP_XOR1>(y);
+  if constexpr (TCN == 16) y += dpp_d<DPP_ROR8>(y);
+  return y;
+}
+__device__ __forceinline__ int trow(int tr, int lane) { return 4 * tr + 2 * ((lane >> 2) & 1) + ((lane >> 1) & 1); }
+template <int TCN>
+__device__ __forceinline__ bool twriter(int lane) { return TCN == 16 ? (lane & 9) == 0 : (lane & 1) == 0; }
+
+// y = M v, v in LDS; returns row trow(tr, lane)'s value
+template <int TCN>
+__device__ __forceinline__ double tile_matvec4(const double (&M)[4][8], const double* v, int tc, int lane) {
+  double vs[8];
+  ld8(vs, v, tc);
+  double acc[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    double a = 0.0, b2 = 0.0;
+#pragma unroll
+    for (int c = 0; c < 8; c += 2) {
+      a = fma(M[r][c], vs[c], a);
+      b2 = fma(M[r][c + 1], vs[c + 1], b2);
+    }
+    acc[r] = a + b2;
+  }
+  return tile_reduce<TCN>(acc, lane);
+}
+
+// z / r column combination: out[r] = sum_k al_k M[r][(C0 + k) & 7]; the R half
+// only where the wave's slot rows hold an active constraint (rlive, wave-uniform)
+template <int C0>
+__device__ __forceinline__ void colcombo(const double (&Pm)[4][8], const double (&Rm)[4][8], int tc, int tcA,
+                                         double a0, double a1, double a2, bool rlive, double (&zq)[4],
+                                         double (&rq)[4]) {
+  const double al0 = (tc == tcA + ((C0 + 0) >> 3)) ? a0 : 0.0;
+  const double al1 = (tc == tcA + ((C0 + 1) >> 3)) ? a1 : 0.0;
+  const double al2 = (tc == tcA + ((C0 + 2) >> 3)) ? a2 : 0.0;
+  constexpr int c0 = C0 & 7, c1 = (C0 + 1) & 7, c2 = (C0 + 2) & 7;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) zq[r] = fma(al2, Pm[r][c2], fma(al1, Pm[r][c1], al0 * Pm[r][c0]));
+  if (rlive) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rq[r] = fma(al2, Rm[r][c2], fma(al1, Rm[r][c1], al0 * Rm[r][c0]));
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rq[r] = 0.0;
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void write_empty_t(int b, int tid, int N, int code, float* u0g, float* Ug, int* statusg,
+                                              int* itersg) {
+  if (tid < 12) u0g[(size_t)b * 12 + tid] = 0.f;
+  if (Ug)
+    for (int k = tid; k < N * 12; k += NT) Ug[(size_t)b * N * 12 + k] = 0.f;
+  if (tid == 0) {
+    if (statusg) statusg[b] = code;
+    if (itersg) itersg[b] = 0;
+  }
+}
+
+// One robot.  A robot exceeding NV is appended to `queue` (when given) for the
+// next capacity class, otherwise reported MPCQP_STATUS_TOO_LARGE.
+template <int NV>
+__device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>& sm, const float* __restrict__ x0g,
+                                            const float* __restrict__ xrefg, const float* __restrict__ contactg,
+                                            const float* __restrict__ feetg, const float* __restrict__ robotg,
+                                            float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg,
+                                            int* __restrict__ itersg, int* __restrict__ queue) {
+  using C = Cfg<NV>;
+  constexpr int NT = C::NT, TCN = C::TCN, CPL = C::CPL, VPL = C::VPL, RPW = C::RPW;
+  const int tid = threadIdx.x;
+  const int lane = tid & (LANES - 1), wave = uni(tid >> 6);
+  const int tr = tid / TCN, tc = tid % TCN;
+  const int N = P.N;
+#ifdef MPCQP_STAMPS
+  unsigned long long stamps_[7];
+  unsigned long long secacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, seclast_ = 0;
+  int seccur_ = 7;
+#endif
+  STAMP(0);
+
+  // ------------------------------------------------ inputs, stance list
+  if (!form_stage<NT>(sm.f, N, b, tid, x0g, xrefg, contactg, feetg, robotg)) {
+    write_empty_t<NT>(b, tid, N, MPCQP_STATUS_NONFINITE, u0g, Ug, statusg, itersg);
+    return;
+  }
+  if (wave == 0) form_stance(sm.f, sm.mt, N, lane);
+  fsync<NT>();
+  const int S = uni(sm.mt.S);
+  const int n = 3 * S, m = 6 * S;
+  if (n > NV) {
+    if (queue) {   // the next capacity class takes it
+      if (tid == 0) queue[4 + atomicAdd(&queue[0], 1)] = b;
+      return;
+    }
+    write_empty_t<NT>(b, tid, N, MPCQP_STATUS_TOO_LARGE, u0g, Ug, statusg, itersg);
+    return;
+  }
+
+  // ------------------------------------------------ formulation (mpcqp_form.h)
+  form_model<NT>(P, sm.f, sm.mt, N, tid);
+  fsync<NT>();
+  if (tid < NV) sm.gv[tid] = tid < n ? form_g(P, sm.f, sm.mt, tid) : 0.0;
+  STAMP(1);
+
+  // row `r` of the lane's H tile (identity padding beyond n)
+  auto hrow = [&](int r, double (&h)[8]) {
+    const int row = 4 * tr + r;
+    const int sa = row < n ? row / 3 : 0;
+    const int ja = sm.mt.foot_t[sa];
+    const int car = 3 * sm.mt.foot_leg[sa] + row % 3;
+    const double r2 = 2.0 * P.r[row < n ? car : 0];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int col = 8 * tc + c;
+      const int sb = col < n ? col / 3 : 0;
+      const double hv = form_h(sm.f, N, ja, car, sm.mt.foot_t[sb], 3 * sm.mt.foot_leg[sb] + col % 3) +
+                        (row == col ? r2 : 0.0);
+      h[c] = (row < n && col < n) ? hv : (row == col ? 1.0 : 0.0);
+    }
+  };
+  double W[4][8];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) W[r][c] = 0.0;
+#pragma unroll 1
+  for (int r = 0; r < 4; ++r) {
+    double h[8];
+    hrow(r, h);
+    static_for<4>([&](auto Rr) {
+      constexpr int rr = decltype(Rr)::value;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) W[rr][c] = (rr == r) ? h[c] : W[rr][c];
+    });
+  }
+  STAMP(2);
+
+  // ------------------------------------------------ W = H^-1 (symmetric sweep)
+  // pivot K = 8 KT + KC: W_ij -= z_i z_j / d, W_iK = z_i / d, W_KK = -1/d (ends at
+  // -H^-1; padding rows/columns >= n never change).  KC compile-time (register
+  // column), KT a runtime loop so the code stays in the instruction cache.
+#pragma unroll 1
+  for (int KT = 0; 8 * KT < n; ++KT) {
+    static_for<8>([&](auto KCc) {
+      constexpr int KC = decltype(KCc)::value;
+      const int K = 8 * KT + KC;
+      if (K < n) {
+        constexpr int KRR = KC & 3;
+        const int KR = 2 * KT + (KC >> 2);
+        double* const zc = sm.zc[KC & 1];
+        if (tc == KT) {
+          d2* pz = reinterpret_cast<d2*>(zc + 4 * tr);
+          pz[0] = d2{W[0][KC], W[1][KC]};
+          pz[1] = d2{W[2][KC], W[3][KC]};
+        }
+        fsync<NT>();
+        double zr[8], zi[4];
+        ld8(zr, zc, tc);
+        ld4(zi, zc, tr);
+        const double inv = rcp_nr(zc[K]);
+        double beta[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) beta[r] = -zi[r] * inv;
+        if (tr == KR) beta[KRR] = inv - 1.0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int c = 0; c < 8; ++c) W[r][c] = fma(beta[r], zr[c], W[r][c]);
+        if (tc == KT) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) W[r][KC] = zi[r] * inv;
+          if (tr == KR) W[KRR][KC] = -inv;
+        }
+      }
+    });
+  }
+  // P = -(sweep result) = H^-1 ; largest diagonal entry (dependency threshold scale)
+  double wd = 0.0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) W[r][c] = -W[r][c];
+  if (tc == (tr >> 1)) {
+    // diagonal entries: column r (even tile row) or 4 + r (odd); blended
+    // arithmetically -- a select between the two would index the tile at run time
+    const double odd = (double)(tr & 1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double dv = fma(odd, W[r][4 + r], (1.0 - odd) * W[r][r]);
+      if (4 * tr + r < n) wd = fmax(wd, dv);
+    }
+  }
+  wd = wave_max_d(wd);
+  if (lane == 0) sm.wmax[wave] = wd;
+  STAMP(3);
+
+  // unconstrained minimiser x = -W g
+  {
+    const double y = tile_matvec4<TCN>(W, sm.gv, tc, lane);
+    if (twriter<TCN>(lane)) sm.vx[trow(tr, lane)] = -y;
+  }
+  fsync<NT>();
+  double wscale = sm.wmax[0];
+#pragma unroll
+  for (int w = 1; w < C::NW; ++w) wscale = fmax(wscale, sm.wmax[w]);
+  wscale = sgpr_d(wscale);
+
+  // ---- per-lane constraint rows c = lane + 64k (redundant in every wave): the
+  // row's foot-step variables start at cz, its cone coefficients at sm.mt.rows[crt]
+  // (re-read from LDS: registers hold the two tiles); s = a_c . x - b_c
+  int cz[CPL], crt[CPL];
+  double s[CPL];
+  auto cdot = [&](const double* v, int k) -> double {
+    const double* a = sm.mt.rows[crt[k]];
+    const double* vf = v + cz[k];
+    return a[0] * vf[0] + a[1] * vf[1] + a[2] * vf[2];
+  };
+  auto cbound = [&](int k) -> double {   // -b_c: ub on the fz <= ub row (mpc.py:257)
+    return crt[k] == 5 ? sm.mt.ub[cz[k] / 3] : 0.0;
+  };
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) {
+    const int c = lane + LANES * k;
+    const bool ok = c < m;
+    cz[k] = ok ? 3 * (c / 6) : 0;
+    crt[k] = ok ? c % 6 : 0;
+    s[k] = ok ? cdot(sm.vx, k) + cbound(k) : INFINITY;
+  }
+  double x[VPL], u[VPL];
+#pragma unroll
+  for (int k = 0; k < VPL; ++k) {
+    x[k] = sm.vx[lane + LANES * k];
+    u[k] = 0.0;
+  }
+  unsigned long long occ[VPL];
+#pragma unroll
+  for (int k = 0; k < VPL; ++k) occ[k] = 0ull;
+  double Rm[4][8];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) Rm[r][c] = 0.0;
+  auto slots_live = [&](int lo) -> bool {   // any occupied slot in [lo, lo + RPW)
+    const unsigned long long w = occ[lo >> 6] >> (lo & 63);
+    return (RPW >= 64 ? w : (w & ((1ull << RPW) - 1))) != 0ull;
+  };
+
+  // ------------------------- Goldfarb-Idnani dual active set, projected form
+  // One flat loop (one loop-carried copy of the register tiles): each pass takes
+  // one step for the pending violated row p (choosing the most violated row when
+  // none is pending); the step either adds p or drops a blocking slot.
+  const int max_iter = P.max_iter > 0 ? P.max_iter : 8 * NV + 64;
+  const double tol = 1e-9;
+  int it = 0;
+  int status = MPCQP_STATUS_OK;
+  int p = -1;                       // pending violated row (uniform)
+  int v0 = 0, tcA = 0, c0 = 0;      // its foot-step's first variable, tile column, register column
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, thr = 0.0, sp = 0.0, up = 0.0;
+  SEC(0);
+  while (true) {
+    if (p < 0) {
+      // most violated row (lowest lane on ties)
+      double bv = s[0];
+      int bk = 0;
+#pragma unroll
+      for (int k = 1; k < CPL; ++k) {
+        bk = s[k] < bv ? k : bk;
+        bv = vmin(bv, s[k]);
+      }
+      double vmn;
+      const int pl = wave_argmin_d(bv, vmn);
+      if (!(vmn < -tol)) break;
+      const int kp = uni(__builtin_amdgcn_readlane(bk, pl));
+      p = pl + LANES * kp;
+      const int rp = p % 6;
+      a0 = sgpr_d(sm.mt.rows[rp][0]);
+      a1 = sgpr_d(sm.mt.rows[rp][1]);
+      a2 = sgpr_d(sm.mt.rows[rp][2]);
+      thr = sgpr_d(1e-12 * (a0 * a0 + a1 * a1 + a2 * a2) * wscale);
+      v0 = 3 * (p / 6);
+      tcA = v0 >> 3;
+      c0 = v0 & 7;
+      sp = sgpr_d(vmn);   // s_p, tracked like s[] (identical arithmetic)
+      up = 0.0;
+    }
+    if (++it > max_iter) {
+      status = MPCQP_STATUS_MAX_ITER;
+      break;
+    }
+    SEC(1);
+    // z = P a_p, r = R a_p: rows 4tr..4tr+3 in the lanes of tile column tcA
+    // (R rows of slots no wave member holds active are zero: skipped)
+    const bool rlive = slots_live(RPW * wave);
+    double zq[4], rq[4];
+    switch (c0) {
+      case 0: colcombo<0>(W, Rm, tc, tcA, a0, a1, a2, rlive, zq, rq); break;
+      case 1: colcombo<1>(W, Rm, tc, tcA, a0, a1, a2, rlive, zq, rq); break;
+      case 2: colcombo<2>(W, Rm, tc, tcA, a0, a1, a2, rlive, zq, rq); break;
+      case 3: colcombo<3>(W, Rm, tc, tcA, a0, a1, a2, rlive, zq, rq); break;
+      case 4: colcombo<4>(W, Rm, tc, tcA, a0, a1, a2, rlive, zq, rq); break;
+      case 5: colcombo<5>(W, Rm, tc, tcA, a0, a1, a2, rlive, zq, rq); break;
+      case 6: colcombo<6>(W, Rm, tc, tcA, a0, a1, a2, rlive, zq, rq); break;
+      default: colcombo<7>(W, Rm, tc, tcA, a0, a1, a2, rlive, zq, rq); break;
+    }
+    if (c0 >= 6) {   // the foot-step straddles tile columns tcA, tcA + 1 (next lane)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        zq[r] += dpp_shl1(zq[r]);
+        rq[r] += dpp_shl1(rq[r]);
+      }
+    }
+    const int buf = it & 1;
+    double* const vz = sm.vz[buf];
+    double* const vr = sm.vr[buf];
+    if (tc == tcA) {
+      st4(vz, tr, zq);
+      st4(vr, tr, rq);
+    }
+    fsync<NT>();
+    SEC(2);
+    // constraint-row steps zs = A z, slot directions r, variable steps
+    double zs[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) zs[k] = cdot(vz, k);
+    double zsp = zs[0];
+#pragma unroll
+    for (int k = 1; k < CPL; ++k) zsp = (k == (p >> 6)) ? zs[k] : zsp;
+    zsp = readlane_d(zsp, p & 63);   // lane p computed a_p . z exactly as zs
+    double rs[VPL], zx[VPL];
+    double rbest = INFINITY;
+    int lk = 0;
+#pragma unroll
+    for (int k = 0; k < VPL; ++k) {
+      rs[k] = vr[lane + LANES * k];
+      zx[k] = vz[lane + LANES * k];
+      const bool mine = (occ[k] >> lane) & 1ull;
+      const double ratio = (mine && rs[k] > 0.0) ? div_nr(u[k], rs[k]) : INFINITY;
+      lk = ratio < rbest ? k : lk;
+      rbest = vmin(rbest, ratio);
+    }
+    // dual step bound t1 (blocking slot l), primal step t2
+    double t1;
+    const int ll = wave_argmin_d(rbest, t1);
+    const int l = ll + LANES * uni(__builtin_amdgcn_readlane(lk, ll));
+    double t2 = INFINITY;
+    if (zsp > thr) t2 = div_nr(-sp, zsp);
+    const bool add = t2 <= t1;
+    const double tstep = add ? t2 : t1;
+    if (!(tstep < INFINITY)) {
+      status = MPCQP_STATUS_INFEASIBLE;
+      break;
+    }
+#pragma unroll
+    for (int k = 0; k < VPL; ++k) {
+      x[k] = fma(tstep, zx[k], x[k]);
+      const bool mine = (occ[k] >> lane) & 1ull;
+      u[k] = mine ? fma(-tstep, rs[k], u[k]) : u[k];
+    }
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) s[k] = fma(tstep, zs[k], s[k]);
+    sp = sgpr_d(fma(tstep, zsp, sp));
+    up = sgpr_d(up + tstep);
+    SEC(add ? 5 : 6);
+    // rank-1 updates  W += aW cv^T,  R += aR cv^T  (rows by the lane's tile row)
+    double aW[4], aR[4], cv[8];
+    int zrow = -1;   // R row to clear (drop)
+    if (add) {
+      // slot q (first free); P -= z z^T / sigma ; R -= (r - e_q) z^T / sigma
+      int q = 0;
+#pragma unroll
+      for (int k = VPL - 1; k >= 0; --k)
+        if (~occ[k]) q = LANES * k + __builtin_ctzll(~occ[k]);
+      const double is = rcp_nr(zsp);
+      double zr4[4], rr4[4];
+      ld4(zr4, vz, tr);
+      ld8(cv, vz, tc);
+      ld4(rr4, vr, tr);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        aW[r] = -zr4[r] * is;
+        aR[r] = ((4 * tr + r == q) ? 1.0 - rr4[r] : -rr4[r]) * is;
+      }
+#pragma unroll
+      for (int k = 0; k < VPL; ++k) u[k] = (lane + LANES * k == q) ? up : u[k];
+      occ[q >> 6] |= 1ull << (q & 63);
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) s[k] = (lane + LANES * k == p) ? 0.0 : s[k];
+      p = -1;
+    } else {
+      // drop slot l: eta = Minv_ll, y = Minv[:, l] = R (H R_l^T)
+      const int lt = l >> 2, lr = l & 3;
+      if (tr == lt) {
+        double row[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) row[c] = lr == 0 ? Rm[0][c] : lr == 1 ? Rm[1][c] : lr == 2 ? Rm[2][c] : Rm[3][c];
+        st8(sm.rl, tc, row);
+      }
+      fsync<NT>();
+      ld8(cv, sm.rl, tc);
+      {
+        double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 1
+        for (int r = 0; r < 4; ++r) {
+          double h[8];
+          hrow(r, h);
+          double a = 0.0;
+#pragma unroll
+          for (int c = 0; c < 8; ++c) a = fma(h[c], cv[c], a);
+          static_for<4>([&](auto Rr) {
+            constexpr int rr = decltype(Rr)::value;
+            acc[rr] = (rr == r) ? a : acc[rr];
+          });
+        }
+        const double tvv = tile_reduce<TCN>(acc, lane);
+        if (twriter<TCN>(lane)) sm.tv[trow(tr, lane)] = tvv;
+      }
+      fsync<NT>();
+      {
+        const double yvv = tile_matvec4<TCN>(Rm, sm.tv, tc, lane);
+        if (twriter<TCN>(lane)) sm.yv[trow(tr, lane)] = yvv;
+      }
+      fsync<NT>();
+      const double ie = rcp_nr(sm.yv[l]);
+      double rl4[4], yv4[4];
+      ld4(rl4, sm.rl, tr);
+      ld4(yv4, sm.yv, tr);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        aW[r] = rl4[r] * ie;     // P += R_l^T R_l / eta
+        aR[r] = -yv4[r] * ie;    // R -= y R_l / eta
+      }
+      zrow = l;
+#pragma unroll
+      for (int k = 0; k < VPL; ++k) u[k] = (lane + LANES * k == l) ? 0.0 : u[k];
+      occ[l >> 6] &= ~(1ull << (l & 63));
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) W[r][c] = fma(aW[r], cv[c], W[r][c]);
+    if (rlive || slots_live(RPW * wave)) {   // this wave's slot rows, before or after the step
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) Rm[r][c] = fma(aR[r], cv[c], Rm[r][c]);
+    }
+    if (zrow >= 0) {
+      if (tr == (zrow >> 2)) {   // clear row l of R exactly
+        const int lr = zrow & 3;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          if (lr == 0) Rm[0][c] = 0.0;
+          if (lr == 1) Rm[1][c] = 0.0;
+          if (lr == 2) Rm[2][c] = 0.0;
+          if (lr == 3) Rm[3][c] = 0.0;
+        }
+      }
+      fsync<NT>();   // the drop buffers are rewritten by the next drop
+    }
+    SEC(0);
+  }
+  SEC(7);
+  STAMP(4);
+
+  // ------------------------------- final x, KKT verification, output
+  if (wave == 0) {
+#pragma unroll
+    for (int k = 0; k < VPL; ++k) sm.vx[lane + LANES * k] = x[k];
+  }
+  fsync<NT>();
+  {
+    int bad = 0;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      if (lane + LANES * k < m) {
+        const double v = cdot(sm.vx, k) + cbound(k);
+        bad |= (v < -1e-6) || !isfinite(v);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < VPL; ++k)
+      if ((occ[k] >> lane) & 1ull) bad |= (u[k] < -1e-9);
+    if (__any(bad) && status == MPCQP_STATUS_OK) status = MPCQP_STATUS_MAX_ITER;
+  }
+  STAMP(5);
+  STAMP(6);
+
+#ifdef MPCQP_STAMPS
+  if (tid == 0 && Ug) {
+    unsigned long long* dst = (unsigned long long*)(Ug + (size_t)b * N * 12);
+    for (int i = 0; i < 7; ++i) dst[i] = stamps_[i];
+    for (int i = 0; i < 8; ++i) dst[8 + i] = secacc_[i];
+  }
+  Ug = nullptr;
+#endif
+  if (wave == 0) {
+    if (lane < 12) {
+      const int sidx = sm.mt.stance_of[lane / 3];
+      u0g[(size_t)b * 12 + lane] = sidx >= 0 ? (float)sm.vx[3 * sidx + lane % 3] : 0.f;
+    }
+    if (Ug) {
+      for (int k = lane; k < N * 12; k += LANES) {
+        const int sidx = sm.mt.stance_of[k / 3];
+        Ug[(size_t)b * N * 12 + k] = sidx >= 0 ? (float)sm.vx[3 * sidx + k % 3] : 0.f;
+      }
+    }
+    if (lane == 0) {
+      if (statusg) statusg[b] = status;
+      if (itersg) itersg[b] = it;
+    }
+  }
+}

@@ -1,0 +1,7 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 300 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests.log 2>&1; echo "tests exit $?" >> gpurun_out/gpu_tests.log
+timeout -k 10 120 python tools/phase_stamps.py 1024 10 > gpurun_out/stamps_c2.txt 2>&1 && \
+timeout -k 10 200 python bench.py --no-cpu > gpurun_out/bench_c2.json 2> gpurun_out/bench_c2.err
+echo done $?

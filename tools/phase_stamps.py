@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.join(ROOT, "pympc-quadruped_amd"))
 from mpcqp import _lib  # noqa: E402
 from mpcqp.synthetic import make_batch  # noqa: E402
 
-PHASES = ["inputs+model+discretise", "g,Y,T", "H rows", "sweep H^-1", "active set", "refine+verify"]
+PHASES = ["inputs, model, Ya/Yb, g", "H tile", "sweep H^-1", "active set", "KKT check", "-"]
 
 
 def main():
@@ -48,9 +48,15 @@ def main():
         print(f"  {name:26s} median {np.median(dts[:, k]):9.0f}  max {dts[:, k].max():9.0f} cycles")
     tot = ts[:, 6] - ts[:, 0]
     print(f"  {'total':26s} median {np.median(tot):9.0f}  max {tot.max():9.0f}")
-    gi = dts[:, 4]
+    gi = dts[:, 3]
     sel = iters > 0
     print(f"  active-set cycles / iteration: median {np.median(gi[sel] / iters[sel]):.0f}")
+    sec = U.cpu().numpy().reshape(B, -1).view(np.uint64)[:, 8:16].astype(np.int64)
+    names = ["argmin p + loop top", "z, r combination + exchange", "zs, ratio tests, step", "-", "-", "add update", "drop update", "-"]
+    tot_it = iters[sel].sum()
+    for k, name in enumerate(names):
+        if name != "-":
+            print(f"  sec {name:20s} cycles/iteration (batch mean) {sec[sel, k].sum() / tot_it:8.0f}")
 
 
 if __name__ == "__main__":
