@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--no-gather", action="store_true", help="skip the end-of-step u0 gather")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--max-iter", type=int, default=0, help="active-set iteration cap (diagnostics only)")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "latest", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -104,7 +105,11 @@ def main():
     nbat = 4
     host = [make_batch(Bpg, N, seed=1000 * (k + 1) + rank, gaits=gaits, robots=robots, tilt_deg=tilt)
             for k in range(nbat)]
-    eng = LinearMpc(horizon=N, robot=robots[0], device=dev)
+    # the caller knows its contact schedules: promise the largest stance count so a
+    # workload that fits the 64-variable class launches only that kernel
+    max_stance = int(max((h["contact"] > 0).reshape(Bpg, -1).sum(1).max() for h in host))
+    eng = LinearMpc(horizon=N, robot=robots[0], device=dev, max_iter=args.max_iter,
+                    max_stance=max_stance if 3 * max_stance <= 64 else 0)
     dev_b = []
     for h in host:
         dev_b.append({k: torch.as_tensor(v).to(dev).contiguous() for k, v in h.items()})

@@ -26,10 +26,15 @@ def rows(pattern):
     return out
 
 
-def counter(run_dir, name):
+def kname(name):
+    return "mpcqp_kernel_128" if "kernel_128" in name else ("mpcqp_kernel_64" if "kernel_64" in name else name)
+
+
+def counter(run_dir, name, kernel):
+    """Per-dispatch values of one counter for one engine kernel."""
     vals = []
     for r in rows(os.path.join(run_dir, "**", "*counter_collection.csv")):
-        if KERNEL in r.get("Kernel_Name", "") and r.get("Counter_Name") == name:
+        if kname(r.get("Kernel_Name", "")) == kernel and r.get("Counter_Name") == name:
             vals.append(float(r["Counter_Value"]))
     return vals
 
@@ -41,10 +46,12 @@ def main():
     for f in glob.glob(os.path.join(src, "kt", "**", "*stats.csv"), recursive=True):
         shutil.copy(f, os.path.join(dst, os.path.basename(f)))
     stats = rows(os.path.join(src, "kt", "**", "*kernel_stats.csv"))
-    eng = [r for r in stats if KERNEL in r["Name"]]
-    avg_ns = float(eng[0]["AverageNs"]) if eng else None
-    fetch = counter(os.path.join(src, "fetch"), "FETCH_SIZE")
-    write = counter(os.path.join(src, "write"), "WRITE_SIZE")
+    kernels = {}
+    for r in stats:
+        if KERNEL in r["Name"]:
+            kernels[kname(r["Name"])] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                                         "total_ns": float(r["TotalDurationNs"])}
+    dominant = max(kernels, key=lambda k: kernels[k]["total_ns"]) if kernels else None
     bench = {}
     try:
         with open(os.path.join(src, "bench_kt.json")) as fh:
@@ -56,16 +63,23 @@ def main():
         if a == "--config" and i + 1 < len(args):
             cfg = args[i + 1]
     batch = bench.get("config", {}).get("batch_per_gpu")
-    fk = sum(fetch) / len(fetch) if fetch else None
-    wk = sum(write) / len(write) if write else None
+    per_kernel = {}
+    for k, st in kernels.items():
+        fetch = counter(os.path.join(src, "fetch"), "FETCH_SIZE", k)
+        write = counter(os.path.join(src, "write"), "WRITE_SIZE", k)
+        fk = sum(fetch) / len(fetch) if fetch else None
+        wk = sum(write) / len(write) if write else None
+        per_kernel[k] = dict(st, fetch_kib_per_launch_raw=fk, write_kib_per_launch=wk,
+                             hbm_bytes_per_launch=(2 * fk * 1024 + wk * 1024) if fk is not None and wk is not None
+                             else None)
+    dom = per_kernel.get(dominant, {})
     entry = {
         "batch": batch,
-        "kernel_avg_ns_rocprof": avg_ns,
+        "dominant_kernel": dominant,
+        "kernel_avg_ns_rocprof": dom.get("avg_ns"),
         "kernel_ms_avg_bench_events": bench.get("kernel_ms_avg"),
-        "fetch_kib_per_launch_raw": fk,
-        "write_kib_per_launch": wk,
-        "hbm_bytes_per_launch": (2 * fk * 1024 + wk * 1024) if fk is not None and wk is not None else None,
-        "hbm_bytes_per_launch_uncorrected": (fk * 1024 + wk * 1024) if fk is not None and wk is not None else None,
+        "hbm_bytes_per_launch": dom.get("hbm_bytes_per_launch"),
+        "kernels": per_kernel,
         "note": "FETCH_SIZE x2 per MI355X_MICROARCH.md (wide-stream calibration; 4-B staging loads are uncalibrated)",
     }
     path = os.path.join(dst, "pmc_traffic.json")

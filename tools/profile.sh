@@ -8,7 +8,7 @@
 set -euo pipefail
 TAG=${1:?tag}; shift
 OUT=gpurun_out/prof_$TAG
-mkdir -p "$OUT" "profiles/$TAG"
+mkdir -p "$OUT" "$OUT/summary"
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- \
   python3 bench.py --no-cpu --steps 20 --warmup 3 "$@" > "$OUT/bench_kt.json"
@@ -16,4 +16,4 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o pmc --output-for
   python3 bench.py --no-cpu --steps 5 --warmup 1 "$@" > "$OUT/bench_fetch.json"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o pmc --output-format csv -- \
   python3 bench.py --no-cpu --steps 5 --warmup 1 "$@" > "$OUT/bench_write.json"
-python3 tools/pmc_summary.py "$OUT" "profiles/$TAG" "$@"
+python3 tools/pmc_summary.py "$OUT" "$OUT/summary" "$@"
