@@ -255,34 +255,28 @@ __global__ __launch_bounds__(Cfg<64>::NT) __attribute__((amdgpu_waves_per_eu(2, 
   solve_robot<64>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, queue);
 }
 
-// Class NV = 128: a persistent grid of 8-wave workgroups drains the queue the
-// first class filled (queue[0] = count, final once this launch starts: same
-// stream).  Each workgroup takes robots from the cursor queue[1] until it runs
-// past the count -- every workgroup reaches that exit.  The last workgroup to
-// finish resets the counters for the next launch (queue[2] = finished workgroups).
+// Class NV = 128: one 8-wave workgroup per queued robot.  The launch has one
+// workgroup per robot of the batch (the host cannot know the queue length without a
+// sync); the ones beyond the queue count exit at once.  The last workgroup to finish
+// resets the counters for the next launch (queue[0] = count, queue[2] = finished
+// workgroups, queue[4..] = robot indices).  Workloads that fit class 64 skip this
+// launch via mpcqp_set_stance_hint.
 __global__ __launch_bounds__(Cfg<128>::NT) void mpcqp_kernel_128(
     KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
     int* __restrict__ queue) {
   __shared__ SharedT<128> sm;
-  __shared__ int next;
   const int tid = threadIdx.x;
+  const int k = blockIdx.x;
   const int cnt = uni(__hip_atomic_load(&queue[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  while (true) {
-    if (tid == 0) next = atomicAdd(&queue[1], 1);
-    __syncthreads();
-    const int k = uni(next);
-    __syncthreads();
-    if (k >= cnt) break;
+  if (k < cnt) {
     const int b = uni(queue[4 + k]);
     solve_robot<128>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, nullptr);
-    __syncthreads();   // sm is reused by the next robot
   }
   if (tid == 0) {
     if (atomicAdd(&queue[2], 1) == (int)gridDim.x - 1) {
       atomicExch(&queue[0], 0);
-      atomicExch(&queue[1], 0);
       atomicExch(&queue[2], 0);
     }
   }
@@ -384,9 +378,7 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch: ") + hipGetErrorString(e));
   if (large) {
-    // persistent: up to 2 robots per CU in flight (LDS / VGPR bound of the class)
-    const int grid = batch < 2 * ctx->ncu ? batch : 2 * ctx->ncu;
-    hipLaunchKernelGGL(mpcqp_kernel_128, dim3(grid), dim3(Cfg<128>::NT), 0, st, kp, x0, xref, contact, feet, robot,
+    hipLaunchKernelGGL(mpcqp_kernel_128, dim3(batch), dim3(Cfg<128>::NT), 0, st, kp, x0, xref, contact, feet, robot,
                        u0, U, (int*)status, (int*)iters, q);
     e = hipGetLastError();
     if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (large): ") + hipGetErrorString(e));

@@ -27,11 +27,11 @@
 // Swing foot-steps are eliminated exactly (their GRFs are 0: ub gives fz <= 0 and
 // the cone gives mu fz >= |fx|, |fy| >= 0), leaving n = 3 * #stance variables.
 
+// Transient formulation scratch (dead once H and g are built)
 struct alignas(16) Form {
   float in[IN_END];              // staged inputs (x0, feet, robot record, contact, xref)
   double K[3][NU];               // inv(I_w)[r_leg]x, float32-rounded (B_c rows 6:9)
   double G[3][NU];               // R_z^T K                            (A_c B_c rows 0:3)
-  d2 Y[NU * NU];                 // {Ya, Yb}[c1][c2]
   double E0[kMaxN][16];          // sum_{t >= j} q_s e_t[s]
   double E1[kMaxN][8];           // sum_{t >= j} t q_s e_t[s]  (s < 6)
   double ii[9];                  // 3x3 work (world inertia, its inverse)
@@ -39,7 +39,13 @@ struct alignas(16) Form {
   double minv;                   // float32(1/m)
 };
 
-// Robot-independent per-robot data every class keeps for the solve.
+// Hessian blocks {Ya, Yb}[c1][c2]: kept for the whole solve (H entries are
+// re-derived from it when a constraint is dropped)
+struct alignas(16) FormY {
+  d2 Y[NU * NU];
+};
+
+// Per-robot data every class keeps for the solve.
 struct alignas(16) RobotMeta {
   double rows[6][3];             // one-sided cone rows a_r (a_r . f >= b_r)
   double ub[4 * kMaxN];          // contact * fz_max per stance foot-step (mpc.py:257)
@@ -131,7 +137,7 @@ __device__ __forceinline__ int form_stance(const Form& f, RobotMeta& mt, int N, 
 
 // Model (float32-faithful), cone rows, Ya/Yb, horizon suffix sums.  All NT threads.
 template <int NT>
-__device__ __forceinline__ void form_model(const KParams& P, Form& f, RobotMeta& mt, int N, int tid) {
+__device__ __forceinline__ void form_model(const KParams& P, Form& f, FormY& fy, RobotMeta& mt, int N, int tid) {
   const float* const rbs = f.in + IN_ROBOT;
   const double h = P.dt;
   // ---- R_z, I_w = float32(float32(R_z I_B) R_z^T), inverse (mpc.py:178-182)
@@ -250,7 +256,7 @@ __device__ __forceinline__ void form_model(const KParams& P, Form& f, RobotMeta&
         ya = fma(P.q[3 + c1 % 3], minv2, ya);
         yb = fma(P.q[9 + c1 % 3], minv2, yb);
       }
-      f.Y[k] = d2{ca * ya, cb * yb};
+      fy.Y[k] = d2{ca * ya, cb * yb};
     }
   }
 }
@@ -269,11 +275,11 @@ __device__ __forceinline__ double form_g(const KParams& P, const Form& f, const 
 }
 
 // H[a][b] from the foot-steps' horizon steps (ja, jb) and input columns (ca, cb)
-__device__ __forceinline__ double form_h(const Form& f, int N, int ja, int ca, int jb, int cb) {
+__device__ __forceinline__ double form_h(const FormY& fy, int N, int ja, int ca, int jb, int cb) {
   const int mx = ja > jb ? ja : jb;
   const int d = ja > jb ? ja - jb : jb - ja;
   const int m = N - mx;
   const int ta = (m * (4 * m * m - 1)) / 3 + 2 * d * m * m;   // exact integer
-  const d2 y = f.Y[ca * NU + cb];
+  const d2 y = fy.Y[ca * NU + cb];
   return 2.0 * fma((double)m, y[1], (double)ta * y[0]);
 }

@@ -36,6 +36,7 @@ struct Cfg {
 template <int NV>
 struct alignas(16) SharedT {
   Form f;
+  FormY fy;
   RobotMeta mt;
   alignas(16) double zc[2][NV];   // sweep pivot column (double-buffered)
   alignas(16) double vz[2][NV];   // z = P a_p (double-buffered by iteration)
@@ -174,7 +175,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   }
 
   // ------------------------------------------------ formulation (mpcqp_form.h)
-  form_model<NT>(P, sm.f, sm.mt, N, tid);
+  form_model<NT>(P, sm.f, sm.fy, sm.mt, N, tid);
   fsync<NT>();
   if (tid < NV) sm.gv[tid] = tid < n ? form_g(P, sm.f, sm.mt, tid) : 0.0;
   STAMP(1);
@@ -190,7 +191,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     for (int c = 0; c < 8; ++c) {
       const int col = 8 * tc + c;
       const int sb = col < n ? col / 3 : 0;
-      const double hv = form_h(sm.f, N, ja, car, sm.mt.foot_t[sb], 3 * sm.mt.foot_leg[sb] + col % 3) +
+      const double hv = form_h(sm.fy, N, ja, car, sm.mt.foot_t[sb], 3 * sm.mt.foot_leg[sb] + col % 3) +
                         (row == col ? r2 : 0.0);
       h[c] = (row < n && col < n) ? hv : (row == col ? 1.0 : 0.0);
     }
