@@ -37,12 +37,14 @@ struct alignas(16) Form {
   double ii[9];                  // 3x3 work (world inertia, its inverse)
   double rz[2];                  // float32(cos yaw), float32(sin yaw)
   double minv;                   // float32(1/m)
+  double q[16];                  // state weights (staged: indexed per lane below)
 };
 
 // Hessian blocks {Ya, Yb}[c1][c2]: kept for the whole solve (H entries are
 // re-derived from it when a constraint is dropped)
 struct alignas(16) FormY {
   d2 Y[NU * NU];
+  double rd2[NU];   // 2 R_ii (input weights; kernel arguments indexed per lane would be memory loads)
 };
 
 // Per-robot data every class keeps for the solve.
@@ -154,6 +156,7 @@ __device__ __forceinline__ void form_model(const KParams& P, Form& f, FormY& fy,
       return (double)rbs[1 + idx];
     };
     if (tid < 9) f.ii[tid] = f32r(rz(i, 0) * ib(0, j) + rz(i, 1) * ib(1, j) + rz(i, 2) * ib(2, j));
+    if (tid < NX) f.q[tid] = P.q[tid];
     if (tid == 0) {
       f.rz[0] = c;
       f.rz[1] = s;
@@ -218,10 +221,11 @@ __device__ __forceinline__ void form_model(const KParams& P, Form& f, FormY& fy,
     f.G[i][col] = rz(0, i) * kk[0] + rz(1, i) * kk[1] + rz(2, i) * kk[2];
   }
   // ---- horizon suffix sums of Q e_t and t Q e_t; thread s (state component)
+  if (tid < NU) fy.rd2[tid] = 2.0 * P.r[tid];
   if (tid >= 64 - 16 && tid < 64 - 16 + NX) {
     const int sc = tid - (64 - 16);
     const float* xin = f.in + IN_X0;
-    const double q = P.q[sc];
+    const double q = f.q[sc];
     // n1 = Nm x0, n2 = Nm^2 x0 (closed form of the 13x13 products)
     double x0s = (double)xin[sc], n1 = 0.0, n2 = 0.0;
     const double g12 = (double)xin[12];
@@ -249,12 +253,12 @@ __device__ __forceinline__ void form_model(const KParams& P, Form& f, FormY& fy,
       double ya = 0.0, yb = 0.0;
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
-        ya = fma(f.G[i][c1] * P.q[i], f.G[i][c2], ya);
-        yb = fma(f.K[i][c1] * P.q[6 + i], f.K[i][c2], yb);
+        ya = fma(f.G[i][c1] * f.q[i], f.G[i][c2], ya);
+        yb = fma(f.K[i][c1] * f.q[6 + i], f.K[i][c2], yb);
       }
       if (c1 % 3 == c2 % 3) {
-        ya = fma(P.q[3 + c1 % 3], minv2, ya);
-        yb = fma(P.q[9 + c1 % 3], minv2, yb);
+        ya = fma(f.q[3 + c1 % 3], minv2, ya);
+        yb = fma(f.q[9 + c1 % 3], minv2, yb);
       }
       fy.Y[k] = d2{ca * ya, cb * yb};
     }

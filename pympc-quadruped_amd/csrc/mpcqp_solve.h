@@ -180,13 +180,24 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   if (tid < NV) sm.gv[tid] = tid < n ? form_g(P, sm.f, sm.mt, tid) : 0.0;
   STAMP(1);
 
-  // row `r` of the lane's H tile (identity padding beyond n)
-  auto hrow = [&](int r, double (&h)[8]) {
+  // row `r` of the lane's H tile (identity padding beyond n); cj / cc: the tile
+  // columns' foot-step horizon step and input column
+  auto hcols = [&](int (&cj)[8], int (&cc)[8]) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int col = 8 * tc + c;
+      const int sb = col < n ? col / 3 : 0;
+      cj[c] = sm.mt.foot_t[sb];
+      cc[c] = 3 * sm.mt.foot_leg[sb] + col % 3;
+    }
+  };
+  // drop-path variant: column descriptors re-read per entry (no extra live registers)
+  auto hrow_slow = [&](int r, double (&h)[8]) {
     const int row = 4 * tr + r;
     const int sa = row < n ? row / 3 : 0;
     const int ja = sm.mt.foot_t[sa];
     const int car = 3 * sm.mt.foot_leg[sa] + row % 3;
-    const double r2 = 2.0 * P.r[row < n ? car : 0];
+    const double r2 = sm.fy.rd2[row < n ? car : 0];
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       const int col = 8 * tc + c;
@@ -196,35 +207,42 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       h[c] = (row < n && col < n) ? hv : (row == col ? 1.0 : 0.0);
     }
   };
+  auto hrow = [&](int r, const int (&cj)[8], const int (&cc)[8], double (&h)[8]) {
+    const int row = 4 * tr + r;
+    const int sa = row < n ? row / 3 : 0;
+    const int ja = sm.mt.foot_t[sa];
+    const int car = 3 * sm.mt.foot_leg[sa] + row % 3;
+    const double r2 = sm.fy.rd2[row < n ? car : 0];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int col = 8 * tc + c;
+      const double hv = form_h(sm.fy, N, ja, car, cj[c], cc[c]) + (row == col ? r2 : 0.0);
+      h[c] = (row < n && col < n) ? hv : (row == col ? 1.0 : 0.0);
+    }
+  };
   double W[4][8];
+  {
+    int cj[8], cc[8];
+    hcols(cj, cc);
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int c = 0; c < 8; ++c) W[r][c] = 0.0;
-#pragma unroll 1
-  for (int r = 0; r < 4; ++r) {
-    double h[8];
-    hrow(r, h);
-    static_for<4>([&](auto Rr) {
-      constexpr int rr = decltype(Rr)::value;
-#pragma unroll
-      for (int c = 0; c < 8; ++c) W[rr][c] = (rr == r) ? h[c] : W[rr][c];
-    });
+    for (int r = 0; r < 4; ++r) hrow(r, cj, cc, W[r]);   // unrolled: rows land in their registers
   }
   STAMP(2);
 
   // ------------------------------------------------ W = H^-1 (symmetric sweep)
   // pivot K = 8 KT + KC: W_ij -= z_i z_j / d, W_iK = z_i / d, W_KK = -1/d (ends at
-  // -H^-1; padding rows/columns >= n never change).  KC compile-time (register
-  // column), KT a runtime loop so the code stays in the instruction cache.
+  // -H^-1; padding rows/columns >= n never change).  One generic rank-1 pass (the
+  // pivot row's coefficient made inv - 1 turns row K into z_j / d), then the pivot
+  // column and diagonal by masked FMAs -- no per-element selects.  KC compile-time
+  // (register column), KT a runtime loop so the code stays in the instruction cache.
 #pragma unroll 1
   for (int KT = 0; 8 * KT < n; ++KT) {
     static_for<8>([&](auto KCc) {
       constexpr int KC = decltype(KCc)::value;
+      constexpr int KRR = KC & 3;
       const int K = 8 * KT + KC;
+      const int KR = 2 * KT + (KC >> 2);
       if (K < n) {
-        constexpr int KRR = KC & 3;
-        const int KR = 2 * KT + (KC >> 2);
         double* const zc = sm.zc[KC & 1];
         if (tc == KT) {
           d2* pz = reinterpret_cast<d2*>(zc + 4 * tr);
@@ -244,11 +262,12 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         for (int r = 0; r < 4; ++r)
 #pragma unroll
           for (int c = 0; c < 8; ++c) W[r][c] = fma(beta[r], zr[c], W[r][c]);
-        if (tc == KT) {
+        // column K: the pass left z_i - z_i d/d ~ 0 there; add z_i / d.  Diagonal:
+        // d/d + 1 -> -1/d.
+        const double cm = (tc == KT) ? inv : 0.0;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) W[r][KC] = zi[r] * inv;
-          if (tr == KR) W[KRR][KC] = -inv;
-        }
+        for (int r = 0; r < 4; ++r) W[r][KC] = fma(zi[r], cm, W[r][KC]);
+        W[KRR][KC] += (tc == KT && tr == KR) ? -inv - 2.0 : 0.0;
       }
     });
   }
@@ -480,7 +499,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll 1
         for (int r = 0; r < 4; ++r) {
           double h[8];
-          hrow(r, h);
+          hrow_slow(r, h);
           double a = 0.0;
 #pragma unroll
           for (int c = 0; c < 8; ++c) a = fma(h[c], cv[c], a);

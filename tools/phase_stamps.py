@@ -51,8 +51,9 @@ def main():
     gi = dts[:, 3]
     sel = iters > 0
     print(f"  active-set cycles / iteration: median {np.median(gi[sel] / iters[sel]):.0f}")
-    sec = U.cpu().numpy().reshape(B, -1).view(np.uint64)[:, 8:16].astype(np.int64)
-    names = ["argmin p + loop top", "z, r combination + exchange", "zs, ratio tests, step", "-", "-", "add update", "drop update", "-"]
+    sec = U.cpu().numpy().reshape(B, -1).view(np.uint64)[:, 8:24].astype(np.int64)
+    names = ["loop top + argmin p", "colcombo", "zs/r gathers", "-", "-", "add: q, 1/s, loads, coefs", "drop path", "-",
+             "a_p setup", "store + barrier", "ratio argmin", "t2, step", "rank-1 FMAs", "-", "-", "-"]
     tot_it = iters[sel].sum()
     for k, name in enumerate(names):
         if name != "-":
