@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define MPCQP_ABI_VERSION 1
+#define MPCQP_ABI_VERSION 2
 #define MPCQP_ROBOT_STRIDE 16
 #define MPCQP_MAX_HORIZON 32
 
@@ -88,6 +88,68 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
 /* Largest number of stance foot-steps the caller promises per robot
  * (0 = unknown: the engine dispatches every capacity class). */
 int mpcqp_set_stance_hint(mpcqp_ctx* ctx, int32_t max_stance);
+
+/* ---- the hot path's callers on the device -------------
+ *
+ * mpcqp_plan replaces, per control iteration and batched over robots:
+ *   ModelPredictiveController.update_robot_state  (state packing)  mpc.py:55-79
+ *     quat2ZYXangle                                                kinematics.py:40-49
+ *   update_mpc_if_needed (desired-pose integrators)                mpc.py:81-92
+ *   generate_reference_trajectory          (MPCQP_PLAN_REFERENCE)  mpc.py:110-170
+ *   Gait.set_iteration / get_gait_table    (MPCQP_PLAN_REFERENCE)  gait.py:76-100
+ * Its x0 / xref / contact outputs feed mpcqp_solve directly (no host round trip).
+ * Call it every control iteration (the integrators run at 1/dt_control) with
+ * flags = MPCQP_PLAN_REFERENCE when iter % iterations_between_mpc == 0 (mpc.py:95),
+ * else 0.  MPCQP_PLAN_NO_INTEGRATE skips the integrators: REFERENCE | NO_INTEGRATE
+ * is generate_reference_trajectory alone (mpc.py:110-170).
+ *
+ *   quat         [B][4]  base orientation (w, x, y, z)            robot_data.quat_base
+ *   pos, omega, vel [B][3]  base position, angular / linear velocity (world)
+ *   rot          [B][3][3]  R_base, row-major (mpc.py:83); NULL = quat2matrix(quat)
+ *                        computed on the device (robot_data.py:75)
+ *   vel_body_des [B][3]  float64 desired base velocity, body frame (mpc.py:83)
+ *   yaw_rate_des [B]     float64 desired yaw rate
+ *   gait         [B][9]  int32: period, stance offsets[4], stance durations[4]
+ *                        (gait.py:16-22; e.g. TROTTING10 = 10, 0 5 5 0, 5 5 5 5);
+ *                        NULL = the caller supplies its own contact schedule
+ *   iteration    [B]     int32 gait segment: floor(iter / iterations_between_mpc) % period
+ *                        (gait.py:76-78)
+ *   height_des   [B]     desired CoM height (robot_configs.py:50,69)
+ *   plan_state   [B][MPCQP_PLAN_STRIDE] float64 in/out: x_des, y_des, yaw_des,
+ *                        roll_init, pitch_init, started, 0, 0; all-zero = first run
+ *   x0 [B][13], xref [B][N][13], contact [B][N][4]: out (xref / contact only written
+ *                        with MPCQP_PLAN_REFERENCE; contact only with a gait)
+ */
+#define MPCQP_PLAN_STRIDE 8
+#define MPCQP_GAIT_STRIDE 9
+#define MPCQP_PLAN_REFERENCE 1
+#define MPCQP_PLAN_NO_INTEGRATE 2
+int mpcqp_plan(mpcqp_ctx* ctx, int32_t batch, int32_t flags, const float* quat, const float* pos,
+               const float* omega, const float* vel, const float* rot, const double* vel_body_des,
+               const double* yaw_rate_des, const int32_t* gait, const int32_t* iteration,
+               const float* height_des, double* plan_state, float* x0, float* xref, float* contact,
+               void* stream);
+
+/* The same, reading Isaac Gym's actor root-state tensor in place:
+ * root_states [B][13] = pos(3), quat(x, y, z, w), lin_vel(3), ang_vel(3) -- the
+ * layout isaacgym_a1.py:119-128 slices and reorders per robot on the host.  R_base
+ * is quat2matrix of that quaternion. */
+int mpcqp_plan_root_states(mpcqp_ctx* ctx, int32_t batch, int32_t flags, const float* root_states,
+                           const double* vel_body_des, const double* yaw_rate_des, const int32_t* gait,
+                           const int32_t* iteration, const float* height_des, double* plan_state, float* x0,
+                           float* xref, float* contact, void* stream);
+
+/* Planner constants: dt_control (linear_mpc_configs.py:6, default 0.001), gravity
+ * (:13, 9.81) and the reference-position clamp (mpc.py:121, 0.1). */
+int mpcqp_set_planner(mpcqp_ctx* ctx, double dt_control, double gravity, double max_pos_error);
+
+/* Stance-leg joint torques tau = Jv_leg^T (-f_leg) (leg_controller.py:86-89,
+ * SURVEY §8 f4) for the legs with stance[b * stance_stride + leg] > 0 -- the
+ * controller's `not swing_states[leg]` (leg_controller.py:77); swing-leg entries of
+ * tau are not written.  jac [B][4][3][3]: each leg's 3x3 block of its foot Jacobian (rows = world
+ * x, y, z; columns = the leg's 3 joints), row-major.  u0 [B][12], tau [B][12]. */
+int mpcqp_stance_torques(mpcqp_ctx* ctx, int32_t batch, const float* jac, const float* stance,
+                         int32_t stance_stride, const float* u0, float* tau, void* stream);
 
 int mpcqp_destroy(mpcqp_ctx* ctx);
 

@@ -241,6 +241,7 @@ __device__ __forceinline__ int wave_argmin_d(double v, double& vmin_out) {
 
 #include "mpcqp_form.h"
 #include "mpcqp_solve.h"
+#include "mpcqp_plan.h"
 
 // Class NV = 64: one 2-wave workgroup per robot of the batch.  Robots with more
 // than 64 stance variables are appended to `queue` (when given) for class 128.
@@ -292,6 +293,9 @@ struct mpcqp_ctx {
   int ncu;
   int qcap;           // robots the device queue can hold
   int* queue;         // [count, next, finished, pad, robots...] for class 128
+  double dt_control;  // planner constants (mpcqp_set_planner)
+  double gravity;
+  double max_pos_error;
   std::string err;
 };
 
@@ -330,6 +334,9 @@ int mpcqp_create(const mpcqp_params* p, int32_t device, mpcqp_ctx** out) {
   ctx->queue = nullptr;
   ctx->qcap = 0;
   ctx->ncu = 0;
+  ctx->dt_control = 0.001;    // linear_mpc_configs.py:6
+  ctx->gravity = 9.81;        // linear_mpc_configs.py:13
+  ctx->max_pos_error = 0.1;   // mpc.py:121
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->ncu = prop.multiProcessorCount;
   if (ctx->ncu <= 0) ctx->ncu = 256;
@@ -383,6 +390,82 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
     e = hipGetLastError();
     if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (large): ") + hipGetErrorString(e));
   }
+  return MPCQP_OK;
+}
+
+int mpcqp_set_planner(mpcqp_ctx* ctx, double dt_control, double gravity, double max_pos_error) {
+  if (!ctx || !(dt_control >= 0.0) || !(max_pos_error >= 0.0)) return MPCQP_ERR_ARG;
+  ctx->dt_control = dt_control;
+  ctx->gravity = gravity;
+  ctx->max_pos_error = max_pos_error;
+  return MPCQP_OK;
+}
+
+static int launch_plan(mpcqp_ctx* ctx, int32_t batch, int32_t flags, int root_layout, const float* quat,
+                       const float* pos, const float* omega, const float* vel, const float* rot,
+                       const double* vel_body_des, const double* yaw_rate_des, const int32_t* gait,
+                       const int32_t* iteration, const float* height_des, double* plan_state, float* x0,
+                       float* xref, float* contact, void* stream) {
+  if (!ctx) return MPCQP_ERR_ARG;
+  if (batch < 0) return set_err(ctx, MPCQP_ERR_ARG, "batch < 0");
+  if (batch == 0) return MPCQP_OK;
+  if (!quat || (!root_layout && (!pos || !omega || !vel)) || !vel_body_des || !yaw_rate_des || !plan_state ||
+      !x0)
+    return set_err(ctx, MPCQP_ERR_ARG, "null planner input/output pointer");
+  if (flags & ~(MPCQP_PLAN_REFERENCE | MPCQP_PLAN_NO_INTEGRATE))
+    return set_err(ctx, MPCQP_ERR_ARG, "unknown planner flags");
+  const int mpc_tick = (flags & MPCQP_PLAN_REFERENCE) ? 1 : 0;
+  if (mpc_tick && (!height_des || !xref))
+    return set_err(ctx, MPCQP_ERR_ARG, "null height/xref pointer on an MPC tick");
+  if (mpc_tick && gait && (!iteration || !contact))
+    return set_err(ctx, MPCQP_ERR_ARG, "gait given without iteration/contact");
+  if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, "hipSetDevice failed");
+  PlanParams pp;
+  pp.N = ctx->params.horizon;
+  pp.mpc_tick = mpc_tick;
+  pp.root_layout = root_layout;
+  pp.integrate = (flags & MPCQP_PLAN_NO_INTEGRATE) ? 0 : 1;
+  pp.dt = ctx->params.dt;
+  pp.dt_control = ctx->dt_control;
+  pp.gravity = ctx->gravity;
+  pp.max_pos_error = ctx->max_pos_error;
+  hipLaunchKernelGGL(mpcqp_plan_kernel, dim3((batch + kPlanRobots - 1) / kPlanRobots), dim3(kPlanThreads), 0,
+                     (hipStream_t)stream, pp, (int)batch, quat, pos, omega, vel, rot, vel_body_des, yaw_rate_des,
+                     gait, iteration, height_des, plan_state, x0, xref, contact);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("plan launch: ") + hipGetErrorString(e));
+  return MPCQP_OK;
+}
+
+int mpcqp_plan(mpcqp_ctx* ctx, int32_t batch, int32_t flags, const float* quat, const float* pos,
+               const float* omega, const float* vel, const float* rot, const double* vel_body_des,
+               const double* yaw_rate_des, const int32_t* gait, const int32_t* iteration,
+               const float* height_des, double* plan_state, float* x0, float* xref, float* contact,
+               void* stream) {
+  return launch_plan(ctx, batch, flags, 0, quat, pos, omega, vel, rot, vel_body_des, yaw_rate_des, gait,
+                     iteration, height_des, plan_state, x0, xref, contact, stream);
+}
+
+int mpcqp_plan_root_states(mpcqp_ctx* ctx, int32_t batch, int32_t flags, const float* root_states,
+                           const double* vel_body_des, const double* yaw_rate_des, const int32_t* gait,
+                           const int32_t* iteration, const float* height_des, double* plan_state, float* x0,
+                           float* xref, float* contact, void* stream) {
+  return launch_plan(ctx, batch, flags, 1, root_states, nullptr, nullptr, nullptr, nullptr, vel_body_des,
+                     yaw_rate_des, gait, iteration, height_des, plan_state, x0, xref, contact, stream);
+}
+
+int mpcqp_stance_torques(mpcqp_ctx* ctx, int32_t batch, const float* jac, const float* contact,
+                         int32_t contact_stride, const float* u0, float* tau, void* stream) {
+  if (!ctx) return MPCQP_ERR_ARG;
+  if (batch < 0 || contact_stride < 4) return set_err(ctx, MPCQP_ERR_ARG, "batch < 0 or contact_stride < 4");
+  if (batch == 0) return MPCQP_OK;
+  if (!jac || !contact || !u0 || !tau) return set_err(ctx, MPCQP_ERR_ARG, "null torque pointer");
+  if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, "hipSetDevice failed");
+  const int threads = (int)batch * 12;
+  hipLaunchKernelGGL(mpcqp_stance_torque_kernel, dim3((threads + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     (int)batch, jac, contact, (int)contact_stride, u0, tau);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("torque launch: ") + hipGetErrorString(e));
   return MPCQP_OK;
 }
 

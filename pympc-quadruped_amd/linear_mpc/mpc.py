@@ -5,11 +5,13 @@ Same module name, class name, constructor and methods as the reference's
 ``scripts/mujoco_aliengo.py`` and ``scripts/isaacgym_a1.py`` run unchanged after
 ``sys.path.append('../linear_mpc'); from mpc import ModelPredictiveController``.
 
-What changes underneath: ``_solve_mpc`` (mpc.py:262-290) no longer builds the
-QP with NumPy/SciPy and solves it with Drake; it hands (x0, X_ref, gait table,
-foot positions, robot parameters) to ``mpcqp.LinearMpc`` which formulates and
-solves on the GPU (include/mpcqp.h).  Nothing here imports pydrake, qpsolvers,
-numba, pinocchio or matplotlib.
+What changes underneath: the planner state (desired x / y / yaw integrators,
+roll / pitch compensation, mpc.py:84-152) lives on the device and is advanced
+by ``mpcqp_plan`` every control iteration; on MPC ticks X_ref is built there
+too and ``_solve_mpc`` (mpc.py:262-290) hands (x0, X_ref, gait table, foot
+positions, robot parameters) to ``mpcqp_solve`` without a host round trip.
+The QP is never built with NumPy/SciPy nor solved with Drake.  Nothing here
+imports pydrake, qpsolvers, numba, pinocchio or matplotlib.
 
 Behaviour kept from the reference:
   * dt = 0.05 regardless of the config (mpc.py:38); the horizon is
@@ -32,7 +34,6 @@ if _PKG not in sys.path:
     sys.path.insert(0, _PKG)
 
 from mpcqp.params import pack_robot  # noqa: E402
-from mpcqp.reference import ReferenceTrajectory  # noqa: E402
 
 
 def quat2ZYXangle(quat):
@@ -73,16 +74,60 @@ class ModelPredictiveController():
             dict(mass=float(self.mass), fz_max=float(self.fz_max), mu=float(self.mu),
                  inertia=np.array([I[0, 0], I[0, 1], I[0, 2], I[1, 1], I[1, 2], I[2, 2]],
                                   dtype=np.float32)))
-        self._ref = ReferenceTrajectory(self.horizon, self.com_height_des, batch=1, dt=self.dt,
-                                        dt_control=self.dt_control, gravity=self.gravity)
 
     def _get_engine(self):
         if self._engine is None:
+            import torch
             from mpcqp import LinearMpc
-            self._engine = LinearMpc(horizon=self.horizon, robot=self._robot_record, dt=self.dt,
-                                     Q=self.q_diag, R=self.r_diag,
-                                     device=os.environ.get("MPCQP_DEVICE", "cuda:0"))
+            from mpcqp._lib import PLAN_STRIDE
+            e = LinearMpc(horizon=self.horizon, robot=self._robot_record, dt=self.dt,
+                          Q=self.q_diag, R=self.r_diag, device=os.environ.get("MPCQP_DEVICE", "cuda:0"))
+            e.set_planner(dt_control=self.dt_control, gravity=self.gravity)
+            d, f32 = e.device, dict(dtype=torch.float32, device=e.device)
+            self._dev = dict(
+                plan_state=torch.zeros((1, PLAN_STRIDE), dtype=torch.float64, device=d),
+                x0=torch.zeros((1, 13), **f32), xref=torch.zeros((1, self.horizon, 13), **f32),
+                height=torch.full((1,), float(self.com_height_des), **f32),
+                robot=torch.as_tensor(self._robot_record).reshape(1, -1).to(d))
+            self._engine = e
         return self._engine
+
+    def _planner_inputs(self):
+        """robot_data -> the planner's device inputs (float32 state, float32 R_base)."""
+        import torch
+        rd = self.__robot_data
+        d = self._engine.device
+        host = np.concatenate([np.asarray(rd.quat_base, dtype=np.float32).reshape(4),
+                               np.asarray(rd.pos_base, dtype=np.float32).reshape(3),
+                               np.asarray(rd.ang_vel_base, dtype=np.float32).reshape(3),
+                               np.asarray(rd.lin_vel_base, dtype=np.float32).reshape(3),
+                               np.asarray(rd.R_base, dtype=np.float32).reshape(9)])
+        t = torch.from_numpy(host).to(d)
+        return dict(quat=t[0:4], pos=t[4:7], omega=t[7:10], vel=t[10:13], rot=t[13:22])
+
+    def _plan(self, flags, vel_base_des_body, yaw_turn_rate):
+        import torch
+        e = self._get_engine()
+        dv = self._dev
+        vb = torch.as_tensor(np.asarray(vel_base_des_body, dtype=np.float64).reshape(1, 3)).to(e.device)
+        yr = torch.full((1,), float(yaw_turn_rate), dtype=torch.float64, device=e.device)
+        e.plan(flags, dv["plan_state"], dv["x0"], vb, yr, height_des=dv["height"], xref=dv["xref"],
+               **self._planner_inputs())
+
+    def _planner_state(self):
+        return self._dev["plan_state"].cpu().numpy()[0]
+
+    @property
+    def xpos_base_desired(self):
+        return float(self._planner_state()[0])
+
+    @property
+    def ypos_base_desired(self):
+        return float(self._planner_state()[1])
+
+    @property
+    def yaw_desired(self):
+        return float(self._planner_state()[2])
 
     # data: [pos_base, vel_base, quat_base, omega_base, ...]   (mpc.py:54-79)
     def update_robot_state(self, robot_data):
@@ -106,40 +151,46 @@ class ModelPredictiveController():
 
     def update_mpc_if_needed(self, iter_counter, base_vel_base_des, yaw_turn_rate_des,
                              gait_table, solver='drake', debug=False, iter_debug=None):
-        """mpc.py:81-108."""
-        vel_base_des = self.__robot_data.R_base @ base_vel_base_des
-        self._ref.integrate_desired(self.yaw, vel_base_des, yaw_turn_rate_des)
-        self.xpos_base_desired = float(self._ref.xpos_des[0])
-        self.ypos_base_desired = float(self._ref.ypos_des[0])
-        self.yaw_desired = float(self._ref.yaw_des[0])
-        self.is_first_run = False
+        """mpc.py:81-108: integrators on the device every call, a solve on MPC ticks."""
+        from mpcqp._lib import PLAN_REFERENCE
+        self._base_vel_base_des = np.asarray(base_vel_base_des, dtype=np.float64).reshape(3)
         if iter_counter % self.iterations_between_mpc == 0:
-            ref_traj = self.generate_reference_trajectory(vel_base_des, yaw_turn_rate_des)
-            self.ref_traj = ref_traj
-            self.__contact_forces = self._solve_mpc(ref_traj, gait_table, solver=solver)[0:12]
+            # integrate + reference trajectory in one launch (mpc.py:84-92, :110-170)
+            self._plan(PLAN_REFERENCE, self._base_vel_base_des, yaw_turn_rate_des)
+            self.is_first_run = False
+            self.__contact_forces = self._solve_mpc(self._dev["xref"], gait_table, solver=solver)[0:12]
+            self.ref_traj = self._dev["xref"].cpu().numpy().reshape(-1)
             if debug and iter_counter == iter_debug:
                 warnings.warn("debug CoM-trajectory plot (mpc.py:293-318) is not provided by the engine")
+        else:
+            self._plan(0, self._base_vel_base_des, yaw_turn_rate_des)
+            self.is_first_run = False
         return self.__contact_forces[0:12]
 
     def generate_reference_trajectory(self, vel_base_des, yaw_turn_rate):
-        """mpc.py:110-170 (stateful clamp + roll/pitch compensation)."""
-        X = self._ref.trajectory(self.current_state[None, :], np.asarray(vel_base_des)[None, :],
-                                 yaw_turn_rate)[0]
-        self.xpos_base_desired = float(self._ref.xpos_des[0])
-        self.ypos_base_desired = float(self._ref.ypos_des[0])
-        self.roll_init = float(self._ref.roll_init[0])
-        self.pitch_init = float(self._ref.pitch_init[0])
-        return X
+        """mpc.py:110-170 alone (stateful clamp + roll/pitch compensation), on the device.
+
+        ``vel_base_des`` is the world-frame command as in the reference; it is mapped
+        back to the body frame for the planner, which applies R_base itself."""
+        from mpcqp._lib import PLAN_NO_INTEGRATE, PLAN_REFERENCE
+        R = np.asarray(self.__robot_data.R_base, dtype=np.float64).reshape(3, 3)
+        vb = np.linalg.solve(R, np.asarray(vel_base_des, dtype=np.float64).reshape(3))
+        self._plan(PLAN_REFERENCE | PLAN_NO_INTEGRATE, vb, yaw_turn_rate)
+        return self._dev["xref"].cpu().numpy().reshape(-1)
 
     def _solve_mpc(self, ref_traj, gait_table, solver='drake', debug=False):
-        """mpc.py:262-290 -> one engine call; returns U[12N] (float64, like Drake)."""
+        """mpc.py:262-290 -> one engine call; returns U[12N] (float64, like Drake).
+
+        x0 is the device state the planner packed this iteration; ``ref_traj`` may be
+        the planner's device X_ref or a host array."""
         assert solver == 'drake' or solver == 'qpsolvers' or solver == 'hip'
+        e = self._get_engine()
         feet = np.asarray([np.asarray(f, dtype=np.float64).reshape(3) for f in self.pos_base_feet],
                           dtype=np.float32)
-        res = self._get_engine().solve(self.current_state[None, :],
-                                       np.asarray(ref_traj, dtype=np.float32)[None, :],
-                                       np.asarray(gait_table, dtype=np.float32)[None, :],
-                                       feet[None, :, :], return_all=True)
+        res = e.solve(self._dev["x0"], ref_traj if not isinstance(ref_traj, np.ndarray)
+                      else np.asarray(ref_traj, dtype=np.float32)[None, :],
+                      np.asarray(gait_table, dtype=np.float32)[None, :], feet[None, :, :],
+                      robot=self._dev["robot"], return_all=True)
         U = res.U.cpu().numpy().reshape(-1).astype(np.float64)
         status = int(res.status.cpu().numpy()[0])
         if status != 0:

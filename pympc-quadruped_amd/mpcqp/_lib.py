@@ -27,7 +27,16 @@ EXPORTED_SYMBOLS = (
     "mpcqp_set_stance_hint",
     "mpcqp_destroy",
     "mpcqp_last_error",
+    "mpcqp_plan",
+    "mpcqp_plan_root_states",
+    "mpcqp_set_planner",
+    "mpcqp_stance_torques",
 )
+ABI_VERSION = 2
+PLAN_STRIDE = 8     # MPCQP_PLAN_STRIDE: float64 planner state per robot
+GAIT_STRIDE = 9     # MPCQP_GAIT_STRIDE: period, offsets[4], durations[4]
+PLAN_REFERENCE = 1      # MPCQP_PLAN_REFERENCE: build X_ref (+ gait table) this tick
+PLAN_NO_INTEGRATE = 2   # MPCQP_PLAN_NO_INTEGRATE: skip the desired-pose integrators
 
 
 class MpcqpParams(ctypes.Structure):
@@ -72,7 +81,15 @@ def load():
     lib.mpcqp_destroy.argtypes = [vp]
     lib.mpcqp_last_error.restype = ctypes.c_char_p
     lib.mpcqp_last_error.argtypes = [vp]
-    if lib.mpcqp_abi_version() != 1:
+    lib.mpcqp_plan.restype = ctypes.c_int
+    lib.mpcqp_plan.argtypes = [vp, i32, i32] + [vp] * 14 + [vp]
+    lib.mpcqp_plan_root_states.restype = ctypes.c_int
+    lib.mpcqp_plan_root_states.argtypes = [vp, i32, i32] + [vp] * 10 + [vp]
+    lib.mpcqp_set_planner.restype = ctypes.c_int
+    lib.mpcqp_set_planner.argtypes = [vp, ctypes.c_double, ctypes.c_double, ctypes.c_double]
+    lib.mpcqp_stance_torques.restype = ctypes.c_int
+    lib.mpcqp_stance_torques.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp]
+    if lib.mpcqp_abi_version() != ABI_VERSION:
         raise MpcqpError("libmpcqp ABI version mismatch")
     _lib = lib
     return lib

@@ -154,3 +154,49 @@ class LinearMpc:
                                     _ptr(feet), _ptr(robot), _ptr(u0), _ptr(U), _ptr(status),
                                     _ptr(iters), ctypes.c_void_p(stream.cuda_stream))
         _lib.check(self._ctx, code, "mpcqp_solve")
+
+    # ---- the hot path's callers on the device (include/mpcqp.h) ----
+
+    def set_planner(self, dt_control=0.001, gravity=9.81, max_pos_error=0.1):
+        """Planner constants (linear_mpc_configs.py:6,13; mpc.py:121)."""
+        _lib.check(self._ctx, self.lib.mpcqp_set_planner(self._ctx, float(dt_control), float(gravity),
+                                                         float(max_pos_error)), "mpcqp_set_planner")
+
+    def plan(self, flags, plan_state, x0, vel_body_des, yaw_rate_des, quat=None, pos=None, omega=None,
+             vel=None, rot=None, root_states=None, gait=None, iteration=None, height_des=None, xref=None,
+             contact=None, stream=None):
+        """One control iteration of state packing + pose integration, and on an MPC
+        tick the reference trajectory and gait table (mpc.py:55-170, gait.py:76-100).
+        ``flags``: True / PLAN_REFERENCE on an MPC tick, PLAN_NO_INTEGRATE to skip the
+        integrators (include/mpcqp.h).
+
+        Every argument is a preallocated contiguous device tensor (float32, except
+        plan_state / vel_body_des / yaw_rate_des float64 and gait / iteration int32);
+        ``root_states`` [B,13] (Isaac Gym layout) replaces quat/pos/omega/vel/rot."""
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        B = int(plan_state.shape[0])
+        s = ctypes.c_void_p(stream.cuda_stream)
+        if root_states is not None:
+            code = self.lib.mpcqp_plan_root_states(
+                self._ctx, B, int(flags), _ptr(root_states), _ptr(vel_body_des), _ptr(yaw_rate_des),
+                _ptr(gait), _ptr(iteration), _ptr(height_des), _ptr(plan_state), _ptr(x0), _ptr(xref),
+                _ptr(contact), s)
+        else:
+            code = self.lib.mpcqp_plan(
+                self._ctx, B, int(flags), _ptr(quat), _ptr(pos), _ptr(omega), _ptr(vel), _ptr(rot),
+                _ptr(vel_body_des), _ptr(yaw_rate_des), _ptr(gait), _ptr(iteration), _ptr(height_des),
+                _ptr(plan_state), _ptr(x0), _ptr(xref), _ptr(contact), s)
+        _lib.check(self._ctx, code, "mpcqp_plan")
+
+    def stance_torques(self, jac, stance, u0, tau, stance_stride=4, stream=None):
+        """tau = Jv_leg^T (-f_leg) for stance legs (leg_controller.py:86-89).
+
+        jac [B,4,3,3] float32 (each leg's 3x3 Jacobian block), stance [B, >=4]
+        (> 0 = stance) read with ``stance_stride``, u0 / tau [B,12]."""
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        B = int(u0.shape[0])
+        code = self.lib.mpcqp_stance_torques(self._ctx, B, _ptr(jac), _ptr(stance), int(stance_stride), _ptr(u0),
+                                             _ptr(tau), ctypes.c_void_p(stream.cuda_stream))
+        _lib.check(self._ctx, code, "mpcqp_stance_torques")

@@ -52,6 +52,26 @@ GAITS = {
 }
 
 
+# Gait enum member names (gait.py:16-22) -> GAITS keys
+GAIT_MEMBERS = {"STANDING": "standing", "TROTTING16": "trot16", "TROTTING10": "trot10",
+                "JUMPING16": "jump16", "PACING16": "pace16", "PACING10": "pace10", "BOUNDING8": "bound8"}
+
+
+def gait_record(gait):
+    """One MPCQP_GAIT_STRIDE record: [period, offsets[4], durations[4]] int32.
+
+    ``gait`` is a GAITS key, a Gait enum member name, or a (period, offsets,
+    durations) triple."""
+    if isinstance(gait, str):
+        period, offsets, durations = GAITS[GAIT_MEMBERS.get(gait, gait)]
+    else:
+        period, offsets, durations = gait
+    rec = np.array([period, *offsets, *durations], dtype=np.int32)
+    if rec.shape != (9,) or rec[0] <= 0:
+        raise ValueError(f"bad gait {gait!r}")
+    return rec
+
+
 def pack_robot(preset, normal=(0.0, 0.0, 1.0), mu=None, fz_max=None):
     """One robot record: [mass, ixx, ixy, ixz, iyy, iyz, izz, mu, fz_max, nx, ny, nz, 0...]."""
     rec = np.zeros(ROBOT_STRIDE, dtype=np.float32)

@@ -14,9 +14,15 @@ SURVEY.md Appendix A), then:
                         every gait member and iterations 0..2*period
   reftraj.npz           generate_reference_trajectory() (mpc.py:110-170) and
                         the update_mpc_if_needed pose integration (mpc.py:83-92)
+  planner.npz           a 45-iteration control sequence through the reference's own
+                        update_robot_state + update_mpc_if_needed (mpc.py:55-108, with
+                        _solve_mpc replaced by a recorder), quat2ZYXangle / quat2matrix
+                        (kinematics.py:40-71) on float32 quaternions, and
+                        LegController.update's stance branch (leg_controller.py:86-89)
 
 Usage:  python tests/golden/make_golden.py            (all horizons, subprocesses)
         python tests/golden/make_golden.py --horizon 10
+        python tests/golden/make_golden.py --planner       (planner.npz only)
 """
 import argparse
 import os
@@ -177,11 +183,105 @@ def gen_reftraj(LinearMpcConfig, robot_configs, mpc):
                         pitch_init=np.array([c_["pitch_init"] for c_ in cases]))
 
 
+class _PlanRobotData:
+    """The RobotData attributes update_robot_state / update_mpc_if_needed /
+    LegController.update read (robot_data.py:59-190), set directly."""
+
+
+def gen_planner():
+    """planner.npz: the reference's own per-iteration planner outputs."""
+    import contextlib
+    import io
+    sys.path[:0] = [ROOT]
+    LinearMpcConfig, robot_configs, mpc, gait = stub_reference(16)
+    import kinematics
+    import leg_controller
+    rng = np.random.default_rng(2024)
+    B, T = 8, 45
+    members = [gait.Gait.TROTTING10, gait.Gait.PACING16, gait.Gait.STANDING, gait.Gait.TROTTING16,
+               gait.Gait.JUMPING16, gait.Gait.PACING10, gait.Gait.TROTTING10, gait.Gait.STANDING]
+    quat = np.zeros((B, T, 4), np.float32)
+    pos = np.zeros((B, T, 3), np.float32)
+    omega = np.zeros((B, T, 3), np.float32)
+    vel = np.zeros((B, T, 3), np.float32)
+    v_body = np.zeros((B, 3))
+    yaw_rate = np.zeros(B)
+    x0 = np.zeros((B, T, 13), np.float32)
+    rot = np.zeros((B, T, 3, 3), np.float32)
+    rpy = np.zeros((B, T, 3))
+    xref = np.zeros((B, 3, 16 * 13), np.float32)
+    table = np.zeros((B, 3, 16 * 4), np.float32)
+    pstate = np.zeros((B, 3, 5))
+    for b in range(B):
+        c = mpc.ModelPredictiveController(LinearMpcConfig, robot_configs.AliengoConfig)
+        v_body[b] = [rng.uniform(-0.5, 1.5), rng.uniform(-0.4, 0.4), 0.0]
+        yaw_rate[b] = rng.uniform(-0.8, 0.8)
+        # a drifting base pose: roll/pitch wobble, a yaw that sweeps past +-pi for some robots
+        rpy0 = np.array([rng.uniform(-0.15, 0.15), rng.uniform(-0.15, 0.15), rng.uniform(-3.1, 3.1)])
+        p0 = np.array([rng.uniform(-1, 1), rng.uniform(-1, 1), 0.38])
+        k_mpc = 0
+        for t in range(T):
+            r, p, y = rpy0 + np.array([0.05 * np.sin(0.3 * t), 0.04 * np.cos(0.2 * t), 0.02 * t])
+            cr, sr, cp, sp, cy, sy = np.cos(r / 2), np.sin(r / 2), np.cos(p / 2), np.sin(p / 2), \
+                np.cos(y / 2), np.sin(y / 2)
+            q = np.array([cr * cp * cy + sr * sp * sy, sr * cp * cy - cr * sp * sy,
+                          cr * sp * cy + sr * cp * sy, cr * cp * sy - sr * sp * cy], dtype=np.float32)
+            quat[b, t] = q
+            # positions drift off the desired track so the +-0.1 clamp engages (mpc.py:129-137)
+            pos[b, t] = p0 + np.array([0.004 * t * (1 + b % 3), -0.003 * t * (b % 2), 0.01 * np.sin(t)])
+            omega[b, t] = rng.uniform(-0.5, 0.5, 3)
+            vel[b, t] = [v_body[b][0] + rng.uniform(-0.3, 0.3), rng.uniform(-0.3, 0.3), rng.uniform(-.1, .1)]
+            rd = _PlanRobotData()
+            rd.quat_base = quat[b, t]
+            rd.pos_base = pos[b, t]
+            rd.ang_vel_base = omega[b, t]
+            rd.lin_vel_base = vel[b, t]
+            rd.R_base = kinematics.quat2matrix(quat[b, t])      # robot_data.py:75
+            rd.pos_base_feet = [np.zeros(3)] * 4
+            rot[b, t] = rd.R_base
+            rpy[b, t] = kinematics.quat2ZYXangle(quat[b, t])
+            members[b].set_iteration(c.iterations_between_mpc, t)
+            gt = members[b].get_gait_table()
+            rec = {}
+            c._solve_mpc = lambda ref, g, solver='drake', debug=False, rec=rec: \
+                (rec.update(ref=ref.copy(), g=np.array(g).copy()), np.zeros(12 * 16))[1]
+            c.update_robot_state(rd)
+            with contextlib.redirect_stdout(io.StringIO()):
+                c.update_mpc_if_needed(t, v_body[b].tolist(), float(yaw_rate[b]), gt)
+            x0[b, t] = c.current_state
+            if t % c.iterations_between_mpc == 0:
+                xref[b, k_mpc] = rec["ref"]
+                table[b, k_mpc] = rec["g"]
+                pstate[b, k_mpc] = [c.xpos_base_desired, c.ypos_base_desired, c.yaw_desired,
+                                    float(c.roll_init), float(c.pitch_init)]
+                k_mpc += 1
+    # stance torques through LegController.update with every leg in stance
+    lc = leg_controller.LegController(np.eye(3), np.eye(3))
+    jv = rng.standard_normal((B, 4, 3, 18)).astype(np.float32)
+    forces = rng.uniform(-40, 120, (B, 12)).astype(np.float32)
+    tau = np.zeros((B, 12), np.float32)
+    for b in range(B):
+        rd = _PlanRobotData()
+        rd.Jv_feet = [jv[b, leg] for leg in range(4)]
+        rd.R_base = np.eye(3)
+        rd.base_vel_base_feet = np.zeros((4, 3))
+        rd.base_pos_base_feet = np.zeros((4, 3))
+        tau[b] = lc.update(rd, forces[b], [0, 0, 0, 0], np.zeros((4, 3)), np.zeros((4, 3)))
+    gait_rec = np.array([[m.num_segment, *m.stance_offsets, *m.stance_durations] for m in members], np.int32)
+    np.savez_compressed(os.path.join(HERE, "planner.npz"), quat=quat, pos=pos, omega=omega, vel=vel,
+                        v_body=v_body, yaw_rate=yaw_rate, x0=x0, rot=rot, rpy=rpy, xref=xref, table=table,
+                        plan_state=pstate, gait=gait_rec, jv=jv, forces=forces, tau=tau, horizon=16,
+                        iterations_between_mpc=20, height=0.38)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--horizon", type=int, default=0)
+    ap.add_argument("--planner", action="store_true")
     a = ap.parse_args()
-    if a.horizon:
+    if a.planner:
+        gen_planner()
+    elif a.horizon:
         gen(a.horizon)
     else:
         for n in HORIZONS:

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     lib = _lib.load()
     for name in _declared():
         assert hasattr(lib, name), name
-    assert lib.mpcqp_abi_version() == 1
+    assert lib.mpcqp_abi_version() == _lib.ABI_VERSION == 2
 
 
 def test_params_struct_layout():
@@ -53,7 +53,33 @@ def test_create_rejects_bad_arguments_without_crashing():
     assert lib.mpcqp_create(ctypes.byref(p), -1, ctypes.byref(ctx)) != 0
     assert lib.mpcqp_solve(None, 1, None, None, None, None, None, None, None, None, None, None) == -1
     assert lib.mpcqp_set_stance_hint(None, 3) == -1
+    assert lib.mpcqp_plan(None, 1, 1, *([None] * 15)) == -1
+    assert lib.mpcqp_plan_root_states(None, 1, 1, *([None] * 11)) == -1
+    assert lib.mpcqp_stance_torques(None, 1, None, None, 4, None, None, None) == -1
+    assert lib.mpcqp_set_planner(None, 0.001, 9.81, 0.1) == -1
     assert lib.mpcqp_destroy(None) == 0
+
+
+def test_header_constants_match_binding():
+    """MPCQP_PLAN_STRIDE / GAIT_STRIDE / plan flags are what the Python side uses."""
+    from mpcqp import _lib
+    src = open(HEADER).read()
+    consts = dict(re.findall(r"#define (MPCQP_\w+) (\d+)", src))
+    assert int(consts["MPCQP_PLAN_STRIDE"]) == _lib.PLAN_STRIDE
+    assert int(consts["MPCQP_GAIT_STRIDE"]) == _lib.GAIT_STRIDE
+    assert int(consts["MPCQP_PLAN_REFERENCE"]) == _lib.PLAN_REFERENCE
+    assert int(consts["MPCQP_PLAN_NO_INTEGRATE"]) == _lib.PLAN_NO_INTEGRATE
+    assert int(consts["MPCQP_ROBOT_STRIDE"]) == _lib.ROBOT_STRIDE
+
+
+def test_gait_records_are_the_reference_gaits():
+    """gait.py:16-22 member names -> [period, offsets, durations]."""
+    from mpcqp.params import gait_record
+    assert gait_record("TROTTING10").tolist() == [10, 0, 5, 5, 0, 5, 5, 5, 5]
+    assert gait_record("PACING16").tolist() == [16, 8, 0, 8, 0, 8, 8, 8, 8]
+    assert gait_record("bound8").tolist() == [8, 4, 4, 0, 0, 4, 4, 4, 4]
+    with pytest.raises(ValueError):
+        gait_record((0, (0, 0, 0, 0), (1, 1, 1, 1)))
 
 
 def test_missing_library_fails_loudly(monkeypatch, tmp_path):

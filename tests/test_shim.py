@@ -70,21 +70,34 @@ def test_shim_surface_and_state_packing():
         c._solve_mpc(np.zeros(130, np.float32), np.ones(40, np.float32), solver="osqp")
 
 
+@pytest.mark.gpu
 def test_shim_reference_trajectory_integration():
+    """The drop-in's planner state lives on the device (mpcqp_plan); its
+    generate_reference_trajectory equals the oracle's (mpc.py:84-92, :110-170)."""
+    from oracle.planner import PlannerOracle
     m = _shim()
     c = m.ModelPredictiveController(LinearMpcConfig, AliengoConfig)
     rd = FakeRobotData()
     c.update_robot_state(rd)
-    c._ModelPredictiveController__robot_data = rd
-    v_world = rd.R_base @ np.array([1.0, 0.0, 0.0])
-    c._ref.integrate_desired(c.yaw, v_world, 0.1)
+    table = np.tile(np.array([1, 0, 0, 1], np.float32), 10)
+    for it in (0, 1, 2, 3):                    # an MPC tick, then integrator-only ticks
+        c.update_mpc_if_needed(it, np.array([1.0, 0.0, 0.0]), 0.1, table)
+    v_world = np.asarray(rd.R_base, np.float32).astype(np.float64) @ np.array([1.0, 0.0, 0.0])
     X = c.generate_reference_trajectory(v_world, 0.1).reshape(10, 13)
     assert X.dtype == np.float32
-    # first tick latches the desired pose at (0, 0) and the clamp pulls it to within 0.1
-    np.testing.assert_allclose(X[0, 3], 0.1 - 0.1, atol=1e-7)
-    np.testing.assert_allclose(np.diff(X[:, 3]), 0.05 * v_world[0], rtol=1e-5)
-    np.testing.assert_allclose(np.diff(X[:, 2]), 0.05 * 0.1, rtol=1e-5)
+    o = PlannerOracle(10, 0.38)
+    o.update_robot_state(np.asarray(rd.quat_base, np.float32), rd.pos_base, rd.ang_vel_base, rd.lin_vel_base)
+    o.integrate(v_world, 0.1)
+    X0 = o.reference_trajectory(v_world, 0.1)
+    np.testing.assert_allclose(c.ref_traj.reshape(10, 13), X0, rtol=0, atol=1e-6)
+    for _ in range(3):
+        o.integrate(v_world, 0.1)
+    np.testing.assert_allclose(X, o.reference_trajectory(v_world, 0.1), rtol=0, atol=1e-6)
+    # the first tick latched x_des = 0, three integrations moved it by 3 ms * v
+    np.testing.assert_allclose(X[0, 3], 0.003 * v_world[0], atol=1e-6)
+    np.testing.assert_allclose(np.diff(X[:, 2]), 0.05 * 0.1, rtol=1e-4)
     assert np.all(X[:, 12] == np.float32(-9.81)) and np.all(X[:, 5] == np.float32(0.38))
+    assert abs(c.xpos_base_desired - o.xpos_des) < 1e-9
 
 
 @pytest.mark.gpu
