@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--max-iter", type=int, default=0, help="active-set iteration cap (diagnostics only)")
+    ap.add_argument("--no-callers", action="store_true", help="skip the planner/torque kernel timing")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "latest", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -75,6 +76,63 @@ def cpu_baseline(bt, N, budget_s):
     if lim is not None:
         lim.unregister() if hasattr(lim, "unregister") else None
     return done / dt, done, dt
+
+
+def time_callers(eng, h, B, N, dev, stream, reps=20):
+    """The hot path's device callers on the same batch, outside the timed region
+    (they are not part of `value`): one MPC-tick mpcqp_plan (Isaac Gym root-state
+    input) and one mpcqp_stance_torques (f4), HIP events on the
+    launch stream; achieved GB/s from mpcqp.roofline.plan_bytes / torque_bytes."""
+    import numpy as np
+    import torch
+    from mpcqp._lib import PLAN_REFERENCE, PLAN_STRIDE
+    from mpcqp.params import gait_record
+    from mpcqp.roofline import PEAK_HBM_GBS, plan_bytes, torque_bytes
+    rng = np.random.default_rng(17)
+    f32 = dict(dtype=torch.float32, device=dev)
+    rs = torch.as_tensor(rng.standard_normal((B, 13)).astype(np.float32)).to(dev)
+    rs[:, 3:7] = torch.nn.functional.normalize(rs[:, 3:7], dim=1)
+    vb = torch.as_tensor(np.tile([0.6, 0.0, 0.0], (B, 1))).to(dev)
+    yr = torch.full((B,), 0.2, dtype=torch.float64, device=dev)
+    gait = torch.as_tensor(np.tile(gait_record("trot10"), (B, 1))).to(dev)
+    it = torch.zeros((B,), dtype=torch.int32, device=dev)
+    hgt = torch.full((B,), 0.42, **f32)
+    state = torch.zeros((B, PLAN_STRIDE), dtype=torch.float64, device=dev)
+    x0 = torch.empty((B, 13), **f32)
+    xref = torch.empty((B, N, 13), **f32)
+    ct = torch.empty((B, N, 4), **f32)
+    jac = torch.as_tensor(rng.standard_normal((B, 4, 3, 3)).astype(np.float32)).to(dev)
+    stance = torch.as_tensor(h["contact"][:, 0, :].copy()).to(dev)
+    u0 = torch.as_tensor(rng.standard_normal((B, 12)).astype(np.float32)).to(dev)
+    tau = torch.zeros((B, 12), **f32)
+
+    def plan():
+        eng.plan(PLAN_REFERENCE, state, x0, vb, yr, root_states=rs, gait=gait, iteration=it,
+                 height_des=hgt, xref=xref, contact=ct, stream=stream)
+
+    def plan_tick():   # a control iteration between MPC ticks: pack + integrate only
+        eng.plan(0, state, x0, vb, yr, root_states=rs, stream=stream)
+
+    def torques():
+        eng.stance_torques(jac, stance, u0, tau, stream=stream)
+
+    out = {}
+    for name, fn, nbytes in (("plan", plan, B * plan_bytes(N, True, True)),
+                             ("plan_between_mpc_ticks", plan_tick, B * plan_bytes(N, False, True)),
+                             ("stance_torques", torques,
+                              B * torque_bytes(float(stance.mean().item())))):
+        for _ in range(3):
+            fn()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for a, b in ev:
+            a.record(stream)
+            fn()
+            b.record(stream)
+        torch.cuda.synchronize(dev)
+        us = sum(a.elapsed_time(b) for a, b in ev) / reps * 1e3
+        gbs = nbytes / (us * 1e-6) / 1e9
+        out[name] = {"us_avg": us, "bytes": nbytes, "achieved_GBs": gbs, "frac_hbm": gbs / PEAK_HBM_GBS}
+    return out
 
 
 def main():
@@ -180,6 +238,8 @@ def main():
     except Exception:
         traffic = None
 
+    callers = None if args.no_callers else time_callers(eng, host[0], Bpg, N, dev, stream)
+
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu:
@@ -214,6 +274,7 @@ def main():
             "iters_mean": float(it_all.mean()),
             "iters_max": int(it_all.max()),
             "status_ok_frac": float((st == 0).mean()),
+            "callers": callers,
         }
         print(json.dumps(line))
     if world > 1:

@@ -52,6 +52,7 @@ __global__ __launch_bounds__(kPlanThreads) void mpcqp_plan_kernel(
     float* __restrict__ x0, float* __restrict__ xref, float* __restrict__ contact) {
 #pragma clang fp contract(off)   // every product and sum rounds, as in NumPy
   __shared__ PlanSeed seed[kPlanRobots];
+  __shared__ float seq[kPlanRobots][3][kMaxN];   // yaw / x / y along the horizon
   const int N = pp.N;
   const int b0 = blockIdx.x * kPlanRobots;
   const int nrob = min(kPlanRobots, B - b0);
@@ -193,52 +194,60 @@ __global__ __launch_bounds__(kPlanThreads) void mpcqp_plan_kernel(
   if (!pp.mpc_tick) return;   // uniform over the workgroup
   __syncthreads();
 
-  // ---- X_ref (mpc.py:154-168) for the workgroup's robots: one contiguous slab
-  const int nx = nrob * N * NX;
-  float* xr = xref + (size_t)b0 * N * NX;
-  for (int e = t; e < nx; e += kPlanThreads) {
-    const int r = e / (N * NX), rem = e - r * (N * NX), i = rem / NX, k = rem - i * NX;
+  // ---- yaw / x / y along the horizon (mpc.py:165-168) accumulate in float32
+  // storage, each step a float64 add rounded: a serial recursion, one thread per
+  // (robot, component), into LDS
+  if (t < 3 * nrob) {
+    const int r = t / 3, c = t - 3 * (t / 3);
     const PlanSeed& sd = seed[r];
-    float v;
-    switch (k) {
-      case 0: v = sd.roll_comp; break;
-      case 1: v = sd.pitch_comp; break;
-      case 2: case 3: case 4: {
-        // yaw / x / y accumulate in float32 storage: each step a float64 add rounded
-        const double step = k == 2 ? sd.rate : (k == 3 ? sd.vx : sd.vy);
-        float a = (float)(k == 2 ? sd.yawd : (k == 3 ? sd.xd : sd.yd));
-        for (int j = 1; j <= i; ++j) a = (float)((double)a + pp.dt * step);
-        v = a;
-        break;
-      }
-      case 5: v = sd.height; break;
-      case 8: v = (float)sd.rate; break;
-      case 9: v = (float)sd.vx; break;
-      case 10: v = (float)sd.vy; break;
-      case 12: v = (float)(-pp.gravity); break;
-      default: v = 0.f;
+    const double step = pp.dt * (c == 0 ? sd.rate : (c == 1 ? sd.vx : sd.vy));
+    float a = (float)(c == 0 ? sd.yawd : (c == 1 ? sd.xd : sd.yd));
+    float* q = seq[r][c];
+    q[0] = a;
+    for (int i = 1; i < N; ++i) {
+      a = (float)((double)a + step);
+      q[i] = a;
     }
-    xr[e] = v;
   }
-  if (gait == nullptr) return;   // the caller supplies its own gait table
+  __syncthreads();
 
-  // ---- gait table (gait.py:81-100): stance when the leg's segment, offset-shifted
-  // into [0, period), is inside its stance duration
-  const int nc = nrob * N * 4;
-  float* ct = contact + (size_t)b0 * N * 4;
-  for (int e = t; e < nc; e += kPlanThreads) {
-    const int r = e / (N * 4), rem = e - r * (N * 4), i = rem >> 2, leg = rem & 3;
+  // ---- X_ref rows (mpc.py:154-168) and gait-table rows (gait.py:81-100): one
+  // thread per (robot, horizon step); a wave's 64 rows are one contiguous range,
+  // so its 13 row stores merge in L2 and the gait row is one 16-byte store
+  const int rows = nrob * N;
+  for (int row = t; row < rows; row += kPlanThreads) {
+    const int r = row / N, i = row - r * N;
     const PlanSeed& sd = seed[r];
+    float* xr = xref + ((size_t)b0 * N + row) * NX;
+    xr[0] = sd.roll_comp;
+    xr[1] = sd.pitch_comp;
+    xr[2] = seq[r][0][i];
+    xr[3] = seq[r][1][i];
+    xr[4] = seq[r][2][i];
+    xr[5] = sd.height;
+    xr[6] = 0.f;
+    xr[7] = 0.f;
+    xr[8] = (float)sd.rate;
+    xr[9] = (float)sd.vx;
+    xr[10] = (float)sd.vy;
+    xr[11] = 0.f;
+    xr[12] = (float)(-pp.gravity);
+    if (gait == nullptr) continue;   // the caller supplies its own gait table
+    // stance when the leg's segment, offset-shifted into [0, period), is inside its
+    // stance duration; a malformed gait (period <= 0) schedules no stance
     const int p = sd.period;
-    float c = 0.f;   // a malformed gait (period <= 0) schedules no stance
+    float c[4] = {0.f, 0.f, 0.f, 0.f};
     if (p > 0) {
       int ih = (i + 1 + sd.ih0) % p;
       if (ih < 0) ih += p;
-      int seg = ih - sd.off[leg];
-      if (seg < 0) seg += p;
-      c = seg < sd.dur[leg] ? 1.f : 0.f;
+#pragma unroll
+      for (int leg = 0; leg < 4; ++leg) {
+        int seg = ih - sd.off[leg];
+        if (seg < 0) seg += p;
+        c[leg] = seg < sd.dur[leg] ? 1.f : 0.f;
+      }
     }
-    ct[e] = c;
+    *reinterpret_cast<float4*>(contact + ((size_t)b0 * N + row) * 4) = make_float4(c[0], c[1], c[2], c[3]);
   }
 }
 

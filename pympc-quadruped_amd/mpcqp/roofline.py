@@ -39,3 +39,23 @@ def executed_flops(N, n, K, q_mean=None):
 def input_bytes(N):
     """HBM bytes per QP: x0, xref, contact, feet, robot in; u0, status, iters out."""
     return 4 * (13 + 13 * N + 4 * N + 12 + 16) + 4 * (12 + 2)
+
+
+def plan_bytes(N, mpc_tick=True, root_layout=False):
+    """HBM bytes per robot of one mpcqp_plan launch (include/mpcqp.h).
+
+    in:  quat/pos/omega/vel (52 B) or one root-state row (52 B), R_base (36 B,
+         separate layout), body command + yaw rate (32 B float64), planner state
+         (48 B), and on an MPC tick height (4 B) + gait record + iteration (40 B);
+    out: x0 (52 B), planner state (48 B), and on an MPC tick X_ref (52 N B) and the
+         gait table (16 N B)."""
+    rd = 52 + (0 if root_layout else 36) + 32 + 48 + (44 if mpc_tick else 0)
+    wr = 52 + 48 + ((52 + 16) * N if mpc_tick else 0)
+    return rd + wr
+
+
+def torque_bytes(stance_frac=1.0):
+    """HBM bytes per robot of mpcqp_stance_torques: stance mask (16 B) read, and for
+    stance legs their 3x3 Jacobian block (36 B) + force (12 B) read, torques (12 B)
+    written."""
+    return 16 + stance_frac * 4 * (36 + 12 + 12)
