@@ -33,10 +33,22 @@ struct Cfg {
   static_assert(NW * LANES * 32 == NV * NV, "4 x 8 tiles");
 };
 
+// Class 64 keeps a copy of H (its register tiles, lane-interleaved) in LDS for the
+// drop path, in the space of the formulation scratch, which is dead once H is
+// built: 32 KB, so that 4 robots still share a CU's 160 KB.  Class 128 has no room
+// and recomputes H entries from Ya / Yb instead.
 template <int NV>
-struct alignas(16) SharedT {
+struct FormArea {
   Form f;
   FormY fy;
+};
+template <int NV>
+struct alignas(16) SharedT {
+  static constexpr bool kHStore = NV == 64;
+  union {
+    FormArea<NV> fa;
+    double ht[kHStore ? NV * NV : 1];   // element e of thread t at ht[e * NT + t]
+  };
   RobotMeta mt;
   alignas(16) double zc[2][NV];   // sweep pivot column (double-buffered)
   alignas(16) double vz[2][NV];   // z = P a_p (double-buffered by iteration)
@@ -157,11 +169,13 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   STAMP(0);
 
   // ------------------------------------------------ inputs, stance list
-  if (!form_stage<NT>(sm.f, N, b, tid, x0g, xrefg, contactg, feetg, robotg)) {
+  Form& smf = sm.fa.f;
+  FormY& smfy = sm.fa.fy;
+  if (!form_stage<NT>(smf, N, b, tid, x0g, xrefg, contactg, feetg, robotg)) {
     write_empty_t<NT>(b, tid, N, MPCQP_STATUS_NONFINITE, u0g, Ug, statusg, itersg);
     return;
   }
-  if (wave == 0) form_stance(sm.f, sm.mt, N, lane);
+  if (wave == 0) form_stance(smf, sm.mt, N, lane);
   fsync<NT>();
   const int S = uni(sm.mt.S);
   const int n = 3 * S, m = 6 * S;
@@ -175,9 +189,9 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   }
 
   // ------------------------------------------------ formulation (mpcqp_form.h)
-  form_model<NT>(P, sm.f, sm.fy, sm.mt, N, tid);
+  form_model<NT>(P, smf, smfy, sm.mt, N, tid);
   fsync<NT>();
-  if (tid < NV) sm.gv[tid] = tid < n ? form_g(P, sm.f, sm.mt, tid) : 0.0;
+  if (tid < NV) sm.gv[tid] = tid < n ? form_g(P, smf, sm.mt, tid) : 0.0;
   STAMP(1);
 
   // row `r` of the lane's H tile (identity padding beyond n); cj / cc: the tile
@@ -197,12 +211,12 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     const int sa = row < n ? row / 3 : 0;
     const int ja = sm.mt.foot_t[sa];
     const int car = 3 * sm.mt.foot_leg[sa] + row % 3;
-    const double r2 = sm.fy.rd2[row < n ? car : 0];
+    const double r2 = smfy.rd2[row < n ? car : 0];
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       const int col = 8 * tc + c;
       const int sb = col < n ? col / 3 : 0;
-      const double hv = form_h(sm.fy, N, ja, car, sm.mt.foot_t[sb], 3 * sm.mt.foot_leg[sb] + col % 3) +
+      const double hv = form_h(smfy, N, ja, car, sm.mt.foot_t[sb], 3 * sm.mt.foot_leg[sb] + col % 3) +
                         (row == col ? r2 : 0.0);
       h[c] = (row < n && col < n) ? hv : (row == col ? 1.0 : 0.0);
     }
@@ -212,11 +226,11 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     const int sa = row < n ? row / 3 : 0;
     const int ja = sm.mt.foot_t[sa];
     const int car = 3 * sm.mt.foot_leg[sa] + row % 3;
-    const double r2 = sm.fy.rd2[row < n ? car : 0];
+    const double r2 = smfy.rd2[row < n ? car : 0];
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       const int col = 8 * tc + c;
-      const double hv = form_h(sm.fy, N, ja, car, cj[c], cc[c]) + (row == col ? r2 : 0.0);
+      const double hv = form_h(smfy, N, ja, car, cj[c], cc[c]) + (row == col ? r2 : 0.0);
       h[c] = (row < n && col < n) ? hv : (row == col ? 1.0 : 0.0);
     }
   };
@@ -226,6 +240,13 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     hcols(cj, cc);
 #pragma unroll
     for (int r = 0; r < 4; ++r) hrow(r, cj, cc, W[r]);   // unrolled: rows land in their registers
+  }
+  if constexpr (SharedT<NV>::kHStore) {
+    fsync<NT>();   // every lane is done reading the formulation scratch H overwrites
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) sm.ht[(8 * r + c) * NT + tid] = W[r][c];
   }
   STAMP(2);
 
@@ -496,17 +517,30 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       ld8(cv, sm.rl, tc);
       {
         double acc[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 1
-        for (int r = 0; r < 4; ++r) {
-          double h[8];
-          hrow_slow(r, h);
-          double a = 0.0;
+        if constexpr (SharedT<NV>::kHStore) {   // the lane's H tile, from LDS
 #pragma unroll
-          for (int c = 0; c < 8; ++c) a = fma(h[c], cv[c], a);
-          static_for<4>([&](auto Rr) {
-            constexpr int rr = decltype(Rr)::value;
-            acc[rr] = (rr == r) ? a : acc[rr];
-          });
+          for (int r = 0; r < 4; ++r) {
+            double a = 0.0, a2 = 0.0;
+#pragma unroll
+            for (int c = 0; c < 8; c += 2) {
+              a = fma(sm.ht[(8 * r + c) * NT + tid], cv[c], a);
+              a2 = fma(sm.ht[(8 * r + c + 1) * NT + tid], cv[c + 1], a2);
+            }
+            acc[r] = a + a2;
+          }
+        } else {
+#pragma unroll 1
+          for (int r = 0; r < 4; ++r) {
+            double h[8];
+            hrow_slow(r, h);
+            double a = 0.0;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) a = fma(h[c], cv[c], a);
+            static_for<4>([&](auto Rr) {
+              constexpr int rr = decltype(Rr)::value;
+              acc[rr] = (rr == r) ? a : acc[rr];
+            });
+          }
         }
         const double tvv = tile_reduce<TCN>(acc, lane);
         if (twriter<TCN>(lane)) sm.tv[trow(tr, lane)] = tvv;
