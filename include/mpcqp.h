@@ -36,7 +36,7 @@
  *   u0      [B][12]    out: first-step GRFs, world frame (mpc.py:99)
  *   U       [B][N][12] out (nullable): the whole optimal input sequence
  *   status  [B]        out (nullable): MPCQP_STATUS_*
- *   iters   [B]        out (nullable): active-set iterations executed
+ *   iters   [B]        out (nullable): active-set steps executed (a pair step counts 2)
  */
 #ifndef MPCQP_H
 #define MPCQP_H

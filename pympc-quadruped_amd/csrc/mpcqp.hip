@@ -239,6 +239,17 @@ __device__ __forceinline__ int wave_argmin_d(double v, double& vmin_out) {
   return l;
 }
 
+// lowest lane holding the f32-rounded wave minimum of v; vmin_out = v in that lane.
+// Not the exact f64 argmin on f32 ties -- for choices where any deterministic
+// near-minimal lane will do (every wave computes the same lane).
+__device__ __forceinline__ int wave_argmin_f32(double v, double& vmin_out) {
+  const float f = (float)v;
+  const float fm = wave_min_f32(f);
+  const int l = uni(__builtin_ctzll(__ballot(f == fm)));
+  vmin_out = readlane_d(v, l);
+  return l;
+}
+
 #include "mpcqp_form.h"
 #include "mpcqp_solve.h"
 #include "mpcqp_plan.h"

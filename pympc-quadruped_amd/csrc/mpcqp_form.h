@@ -55,6 +55,7 @@ struct alignas(16) RobotMeta {
   int foot_leg[4 * kMaxN];       // stance foot-step -> leg
   int stance_of[4 * kMaxN];      // (step, leg) -> stance foot-step or -1
   int S;
+  int fz0_implied;               // mu > 0: the n.f >= 0 row is the half-sum of rows 0 and 1
 };
 
 template <int NT>
@@ -204,6 +205,7 @@ __device__ __forceinline__ void form_model(const KParams& P, Form& f, FormY& fy,
                      : rr == 3 ? -t2k + mu * nk
                      : rr == 4 ? nk : -nk;
     mt.rows[rr][k] = val;
+    if (k18 == 0) mt.fz0_implied = mu > 0.0;
   }
   fsync<NT>();
   // ---- K = float32(inv(I_w) [r]x) (mpc.py:188-189) and G = R_z^T K; thread (i, col)

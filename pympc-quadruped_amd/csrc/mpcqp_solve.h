@@ -45,16 +45,32 @@ struct FormArea {
 template <int NV>
 struct alignas(16) SharedT {
   static constexpr bool kHStore = NV == 64;
+#ifdef MPCQP_NO_PAIR
+  static constexpr bool kPair = false;
+#else
+  static constexpr bool kPair = NV == 64;   // class 128 has no VGPRs to spare for pair steps
+#endif
   union {
     FormArea<NV> fa;
     double ht[kHStore ? NV * NV : 1];   // element e of thread t at ht[e * NT + t]
   };
   RobotMeta mt;
-  alignas(16) double zc[2][NV];   // sweep pivot column (double-buffered)
-  alignas(16) double vz[2][NV];   // z = P a_p (double-buffered by iteration)
+  union {
+    struct {
+      alignas(16) double zc[2][NV];   // sweep pivot column (double-buffered); in the loop:
+                                      // z2 = P a_p2 of a pair step (double-buffered)
+      alignas(16) double vz[2][NV];   // z = P a_p (double-buffered by iteration)
+    };
+    double wb[4 * NV];   // between sweep and loop: W's 3x3 foot-step blocks (9 S <= 4 NV)
+  };
   alignas(16) double vr[2][NV];   // r = R a_p (slot-indexed)
-  alignas(16) double vx[NV];      // x
-  alignas(16) double gv[NV];      // g
+  union {
+    struct {
+      alignas(16) double vx[NV];  // x (before and after the loop)
+      alignas(16) double gv[NV];  // g (before the loop)
+    };
+    alignas(16) double vr2[2][NV];   // in the loop: r2 = R a_p2 of a pair step
+  };
   alignas(16) double rl[NV];      // drop path: R_l, H R_l^T, R H R_l^T
   alignas(16) double tv[NV];
   alignas(16) double yv[NV];
@@ -310,6 +326,15 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   }
   wd = wave_max_d(wd);
   if (lane == 0) sm.wmax[wave] = wd;
+  // the foot-steps' 3x3 diagonal blocks of W, for the rows' dual-curvature scales below
+  fsync<NT>();   // every lane is done reading the last pivot column (wb aliases zc)
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int row = 4 * tr + r, col = 8 * tc + c;
+      if (row < n && col < n && row / 3 == col / 3) sm.wb[9 * (row / 3) + 3 * (row % 3) + col % 3] = W[r][c];
+    }
   STAMP(3);
 
   // unconstrained minimiser x = -W g
@@ -325,9 +350,14 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 
   // ---- per-lane constraint rows c = lane + 64k (redundant in every wave): the
   // row's foot-step variables start at cz, its cone coefficients at sm.mt.rows[crt]
-  // (re-read from LDS: registers hold the two tiles); s = a_c . x - b_c
+  // (re-read from LDS: registers hold the two tiles); s = a_c . x - b_c.
+  // Row choice: the violated row with the most negative s_c / sqrt(a_c^T W a_c)
+  // (violation in the dual metric), which needs fewer add/drop cycles than the
+  // raw most-violated rule.  With mu > 0 the n.f >= 0 row is implied by the two
+  // opposite t1 rows and never enters (s = +inf): it only adds degenerate steps
+  // at the cone apex.  Neither choice changes the (unique) optimum.
   int cz[CPL], crt[CPL];
-  double s[CPL];
+  double s[CPL], rn[CPL];
   auto cdot = [&](const double* v, int k) -> double {
     const double* a = sm.mt.rows[crt[k]];
     const double* vf = v + cz[k];
@@ -342,7 +372,14 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     const bool ok = c < m;
     cz[k] = ok ? 3 * (c / 6) : 0;
     crt[k] = ok ? c % 6 : 0;
-    s[k] = ok ? cdot(sm.vx, k) + cbound(k) : INFINITY;
+    const bool live = ok && !(crt[k] == 4 && sm.mt.fz0_implied);
+    s[k] = live ? cdot(sm.vx, k) + cbound(k) : INFINITY;
+    const double* a = sm.mt.rows[crt[k]];
+    const double* w = sm.wb + 3 * cz[k];
+    double q = 0.0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) q = fma(a[i], fma(w[3 * i], a[0], fma(w[3 * i + 1], a[1], w[3 * i + 2] * a[2])), q);
+    rn[k] = ok && q > 0.0 ? __builtin_amdgcn_rsq(q) : 1.0;
   }
   double x[VPL], u[VPL];
 #pragma unroll
@@ -350,6 +387,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     x[k] = sm.vx[lane + LANES * k];
     u[k] = 0.0;
   }
+  fsync<NT>();   // wb, vx and gv are dead: the loop reuses zc / vz / vr2
   unsigned long long occ[VPL];
 #pragma unroll
   for (int k = 0; k < VPL; ++k) occ[k] = 0ull;
@@ -376,19 +414,29 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, thr = 0.0, sp = 0.0, up = 0.0;
   SEC(0);
   while (true) {
+    // pair candidate p2 (another foot-step's most violated row), set on a fresh choice
+    int p2 = -1, tcA2 = 0, c02 = 0;
+    double b0 = 0.0, b1 = 0.0, b2 = 0.0, thr2 = 0.0, sp2 = 0.0;
     if (p < 0) {
-      // most violated row (lowest lane on ties)
-      double bv = s[0];
+      // most violated row in the dual metric (f32-rounded keys, lowest lane on ties)
+      double key[CPL];
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) key[k] = s[k] < -tol ? s[k] * rn[k] : INFINITY;
+      double bv = key[0];
       int bk = 0;
 #pragma unroll
       for (int k = 1; k < CPL; ++k) {
-        bk = s[k] < bv ? k : bk;
-        bv = vmin(bv, s[k]);
+        bk = key[k] < bv ? k : bk;
+        bv = vmin(bv, key[k]);
       }
-      double vmn;
-      const int pl = wave_argmin_d(bv, vmn);
-      if (!(vmn < -tol)) break;
+      double kmn;
+      const int pl = wave_argmin_f32(bv, kmn);
+      if (!(kmn < INFINITY)) break;
       const int kp = uni(__builtin_amdgcn_readlane(bk, pl));
+      double sv = s[0];
+#pragma unroll
+      for (int k = 1; k < CPL; ++k) sv = (k == kp) ? s[k] : sv;
+      const double vmn = readlane_d(sv, pl);
       p = pl + LANES * kp;
       const int rp = p % 6;
       a0 = sgpr_d(sm.mt.rows[rp][0]);
@@ -400,6 +448,35 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       c0 = v0 & 7;
       sp = sgpr_d(vmn);   // s_p, tracked like s[] (identical arithmetic)
       up = 0.0;
+      // second candidate: the best row of any other foot-step
+      if constexpr (SharedT<NV>::kPair) {
+      double bw = INFINITY;
+      int bk2 = 0;
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const double kk = cz[k] == v0 ? INFINITY : key[k];
+        bk2 = kk < bw ? k : bk2;
+        bw = vmin(bw, kk);
+      }
+      double kmn2;
+      const int ql = wave_argmin_f32(bw, kmn2);
+      if (kmn2 < INFINITY) {
+        const int kq = uni(__builtin_amdgcn_readlane(bk2, ql));
+        double sv2 = s[0];
+#pragma unroll
+        for (int k = 1; k < CPL; ++k) sv2 = (k == kq) ? s[k] : sv2;
+        sp2 = sgpr_d(readlane_d(sv2, ql));
+        p2 = ql + LANES * kq;
+        const int rq = p2 % 6;
+        b0 = sgpr_d(sm.mt.rows[rq][0]);
+        b1 = sgpr_d(sm.mt.rows[rq][1]);
+        b2 = sgpr_d(sm.mt.rows[rq][2]);
+        thr2 = sgpr_d(1e-12 * (b0 * b0 + b1 * b1 + b2 * b2) * wscale);
+        const int w0 = 3 * (p2 / 6);
+        tcA2 = w0 >> 3;
+        c02 = w0 & 7;
+      }
+      }
     }
     if (++it > max_iter) {
       status = MPCQP_STATUS_MAX_ITER;
@@ -409,31 +486,39 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     // z = P a_p, r = R a_p: rows 4tr..4tr+3 in the lanes of tile column tcA
     // (R rows of slots no wave member holds active are zero: skipped)
     const bool rlive = slots_live(RPW * wave);
-    double zq[4], rq[4];
-    switch (c0) {
-      case 0: colcombo<0>(W, Rm, tc, tcA, a0, a1, a2, rlive, zq, rq); break;
-      case 1: colcombo<1>(W, Rm, tc, tcA, a0, a1, a2, rlive, zq, rq); break;
-      case 2: colcombo<2>(W, Rm, tc, tcA, a0, a1, a2, rlive, zq, rq); break;
-      case 3: colcombo<3>(W, Rm, tc, tcA, a0, a1, a2, rlive, zq, rq); break;
-      case 4: colcombo<4>(W, Rm, tc, tcA, a0, a1, a2, rlive, zq, rq); break;
-      case 5: colcombo<5>(W, Rm, tc, tcA, a0, a1, a2, rlive, zq, rq); break;
-      case 6: colcombo<6>(W, Rm, tc, tcA, a0, a1, a2, rlive, zq, rq); break;
-      default: colcombo<7>(W, Rm, tc, tcA, a0, a1, a2, rlive, zq, rq); break;
-    }
-    if (c0 >= 6) {   // the foot-step straddles tile columns tcA, tcA + 1 (next lane)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        zq[r] += dpp_shl1(zq[r]);
-        rq[r] += dpp_shl1(rq[r]);
+    // rows 4tr..4tr+3 of P a and R a for a row a of the foot-step at variable
+    // 8 tA + cA, stored by the lanes of tile column tA
+    auto combo_store = [&](int cA, int tA, double e0, double e1, double e2, double* dz, double* dr) {
+      double zq[4], rq[4];
+      switch (cA) {
+        case 0: colcombo<0>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+        case 1: colcombo<1>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+        case 2: colcombo<2>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+        case 3: colcombo<3>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+        case 4: colcombo<4>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+        case 5: colcombo<5>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+        case 6: colcombo<6>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+        default: colcombo<7>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
       }
-    }
+      if (cA >= 6) {   // the foot-step straddles tile columns tA, tA + 1 (next lane)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          zq[r] += dpp_shl1(zq[r]);
+          rq[r] += dpp_shl1(rq[r]);
+        }
+      }
+      if (tc == tA) {
+        st4(dz, tr, zq);
+        st4(dr, tr, rq);
+      }
+    };
     const int buf = it & 1;
     double* const vz = sm.vz[buf];
     double* const vr = sm.vr[buf];
-    if (tc == tcA) {
-      st4(vz, tr, zq);
-      st4(vr, tr, rq);
-    }
+    double* const vz2 = sm.zc[buf];
+    double* const vr2 = sm.vr2[buf];
+    combo_store(c0, tcA, a0, a1, a2, vz, vr);
+    if (p2 >= 0) combo_store(c02, tcA2, b0, b1, b2, vz2, vr2);
     fsync<NT>();
     SEC(2);
     // constraint-row steps zs = A z, slot directions r, variable steps
@@ -444,6 +529,113 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
     for (int k = 1; k < CPL; ++k) zsp = (k == (p >> 6)) ? zs[k] : zsp;
     zsp = readlane_d(zsp, p & 63);   // lane p computed a_p . z exactly as zs
+
+    // ---- pair step: add p and p2 together when the equality-constrained solution
+    // on A + {p, p2} keeps every multiplier positive.  With Z = [z, z2] and the 2x2
+    // S = [a_p a_p2]^T Z, t = -S^-1 (s_p, s_p2): x += Z t, u_A -= [r r2] t,
+    // u_{p,p2} = t, P -= Z S^-1 Z^T, R -= ([r r2] - E) S^-1 Z^T.  (x, A + {p, p2}) is
+    // then a valid dual active-set iterate (KKT of the sub-problem, u >= 0), so the
+    // method's convergence argument is unchanged; otherwise p takes the usual step.
+    if (p2 >= 0) {
+      double zs2[CPL];
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) zs2[k] = cdot(vz2, k);
+      double v12 = zs2[0], v22 = zs2[0];
+#pragma unroll
+      for (int k = 1; k < CPL; ++k) {
+        v12 = (k == (p >> 6)) ? zs2[k] : v12;
+        v22 = (k == (p2 >> 6)) ? zs2[k] : v22;
+      }
+      const double s12 = sgpr_d(readlane_d(v12, p & 63));    // a_p . z2
+      const double s22 = sgpr_d(readlane_d(v22, p2 & 63));   // a_p2 . z2
+      const double det = zsp * s22 - s12 * s12;
+      bool ok = zsp > thr && s22 > thr2 && det > thr2 * zsp;
+      double tp = 0.0, tq = 0.0, id = 0.0;
+      if (ok) {
+        id = rcp_nr(det);
+        tp = sgpr_d((s12 * sp2 - s22 * sp) * id);
+        tq = sgpr_d((s12 * sp - zsp * sp2) * id);
+        ok = tp > 0.0 && tq > 0.0;
+      }
+      double rs1[VPL], rs2[VPL];
+      int bad = 0;
+#pragma unroll
+      for (int k = 0; k < VPL; ++k) {
+        rs1[k] = vr[lane + LANES * k];
+        rs2[k] = vr2[lane + LANES * k];
+        const bool mine = (occ[k] >> lane) & 1ull;
+        bad |= mine && fma(-tq, rs2[k], fma(-tp, rs1[k], u[k])) < 0.0;
+      }
+      if (ok && !__any(bad)) {
+#pragma unroll
+        for (int k = 0; k < VPL; ++k) {
+          const double zx1 = vz[lane + LANES * k], zx2 = vz2[lane + LANES * k];
+          x[k] = fma(tq, zx2, fma(tp, zx1, x[k]));
+          const bool mine = (occ[k] >> lane) & 1ull;
+          u[k] = mine ? fma(-tq, rs2[k], fma(-tp, rs1[k], u[k])) : u[k];
+        }
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+          const int c = lane + LANES * k;
+          s[k] = (c == p || c == p2) ? 0.0 : fma(tq, zs2[k], fma(tp, zs[k], s[k]));
+        }
+        // slots qa < qb: the first two free ones
+        int qa = 0, qb = 0;
+        {
+          unsigned long long f0 = ~occ[0];
+          if constexpr (VPL == 1) {
+            qa = __builtin_ctzll(f0);
+            qb = __builtin_ctzll(f0 & (f0 - 1));
+          } else {
+            const unsigned long long f1 = ~occ[1];
+            qa = f0 ? __builtin_ctzll(f0) : LANES + __builtin_ctzll(f1);
+            const unsigned long long g0 = f0 & (f0 - 1);
+            qb = g0 ? __builtin_ctzll(g0) : LANES + __builtin_ctzll(f0 ? f1 : (f1 & (f1 - 1)));
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < VPL; ++k) {
+          const int sl = lane + LANES * k;
+          u[k] = sl == qa ? tp : (sl == qb ? tq : u[k]);
+        }
+        occ[qa >> 6] |= 1ull << (qa & 63);
+        occ[qb >> 6] |= 1ull << (qb & 63);
+        // rank-2 updates: row coefficients (al, be) = S^-1 (row's pair), then
+        // M[r][c] -= al cz1[c] + be cz2[c]
+        const double i11 = s22 * id, i12 = -s12 * id, i22 = zsp * id;
+        double cz1[8], cz2[8], z41[4], z42[4];
+        ld8(cz1, vz, tc);
+        ld8(cz2, vz2, tc);
+        ld4(z41, vz, tr);
+        ld4(z42, vz2, tr);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double al = fma(i11, z41[r], i12 * z42[r]);
+          const double be = fma(i12, z41[r], i22 * z42[r]);
+#pragma unroll
+          for (int c = 0; c < 8; ++c) W[r][c] = fma(-be, cz2[c], fma(-al, cz1[c], W[r][c]));
+        }
+        if (rlive || slots_live(RPW * wave)) {
+          double r41[4], r42[4];
+          ld4(r41, vr, tr);
+          ld4(r42, vr2, tr);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int sl = 4 * tr + r;
+            const double e1 = r41[r] - (sl == qa ? 1.0 : 0.0);
+            const double e2 = r42[r] - (sl == qb ? 1.0 : 0.0);
+            const double al = fma(i11, e1, i12 * e2);
+            const double be = fma(i12, e1, i22 * e2);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) Rm[r][c] = fma(-be, cz2[c], fma(-al, cz1[c], Rm[r][c]));
+          }
+        }
+        p = -1;
+        ++it;   // a pair step counts as the two additions it makes
+        SEC(0);
+        continue;
+      }
+    }
     double rs[VPL], zx[VPL];
     double rbest = INFINITY;
     int lk = 0;
@@ -594,6 +786,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   STAMP(4);
 
   // ------------------------------- final x, KKT verification, output
+  fsync<NT>();   // vx aliases the loop's vr2: every wave is done reading it
   if (wave == 0) {
 #pragma unroll
     for (int k = 0; k < VPL; ++k) sm.vx[lane + LANES * k] = x[k];

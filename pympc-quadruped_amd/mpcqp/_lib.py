@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmpcqp.so")
+# MPCQP_LIB: diagnostic override (A/B builds); the default is the in-tree build
+LIB_PATH = os.environ.get("MPCQP_LIB") or os.path.join(_HERE, "libmpcqp.so")
 
 MPCQP_OK = 0
 STATUS_OK = 0

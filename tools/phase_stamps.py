@@ -23,12 +23,14 @@ def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
     N = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     gaits = tuple(sys.argv[3].split(",")) if len(sys.argv) > 3 else ("trot10",)
-    _lib.LIB_PATH = os.path.join(ROOT, "pympc-quadruped_amd", "mpcqp", "libmpcqp_stamps.so")
+    seed = int(sys.argv[4]) if len(sys.argv) > 4 else 1000
+    _lib.LIB_PATH = os.environ.get("MPCQP_STAMPS_LIB") or os.path.join(ROOT, "pympc-quadruped_amd", "mpcqp",
+                                                                       "libmpcqp_stamps.so")
     lib = _lib.load()
     p = _lib.default_params(N)
     ctx = ctypes.c_void_p()
     _lib.check(None, lib.mpcqp_create(ctypes.byref(p), 0, ctypes.byref(ctx)), "create")
-    bt = make_batch(B, N, seed=1000, gaits=gaits, robots=("a1",))
+    bt = make_batch(B, N, seed=seed, gaits=gaits, robots=("a1",))
     dev = torch.device("cuda:0")
     d = {k: torch.as_tensor(v).to(dev).contiguous() for k, v in bt.items()}
     u0 = torch.empty((B, 12), device=dev)
@@ -48,6 +50,8 @@ def main():
         print(f"  {name:26s} median {np.median(dts[:, k]):9.0f}  max {dts[:, k].max():9.0f} cycles")
     tot = ts[:, 6] - ts[:, 0]
     print(f"  {'total':26s} median {np.median(tot):9.0f}  max {tot.max():9.0f}")
+    for i in np.argsort(tot)[-4:]:
+        print(f"  slow robot {i}: total {tot[i]} iterations {iters[i]} phases {dts[i, :5].tolist()}")
     gi = dts[:, 3]
     sel = iters > 0
     print(f"  active-set cycles / iteration: median {np.median(gi[sel] / iters[sel]):.0f}")
