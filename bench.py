@@ -48,8 +48,9 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(bt, N, budget_s):
-    """Reference-faithful NumPy formulation + exact float64 QP solve, 1 core."""
+def cpu_baseline(bt, N, budget_s, rows=None):
+    """Reference-faithful NumPy formulation + exact float64 QP solve, 1 core
+    (robots `rows` of the batch, default all)."""
     try:
         from threadpoolctl import threadpool_limits
         lim = threadpool_limits(1)
@@ -58,10 +59,9 @@ def cpu_baseline(bt, N, budget_s):
     from oracle import formulation as F
     from oracle import qp as Q
     import numpy as np
-    B = bt["x0"].shape[0]
     t0 = time.perf_counter()
     done = 0
-    for b in range(B):
+    for b in (range(bt["x0"].shape[0]) if rows is None else rows):
         rec = bt["robot"][b]
         inertia = np.array([[rec[1], rec[2], rec[3]], [rec[2], rec[4], rec[5]],
                             [rec[3], rec[5], rec[6]]], dtype=np.float32)
@@ -76,6 +76,52 @@ def cpu_baseline(bt, N, budget_s):
     if lim is not None:
         lim.unregister() if hasattr(lim, "unregister") else None
     return done / dt, done, dt
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown CPU"
+
+
+def _cpu_worker(job):
+    bt, N, budget_s, rows = job
+    return cpu_baseline(bt, N, budget_s, rows)
+
+
+def cpu_baseline_all_cores(bt, N, budget_s):
+    """The same CPU port on every host core this job may use (one process per core,
+    robots dealt round-robin).  Rate = robots solved / slowest worker's
+    solve time (process start-up excluded)."""
+    import multiprocessing as mp
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    procs = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", "16")), 16))
+    B = bt["x0"].shape[0]
+    env_keep = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")}
+    for k in env_keep:
+        os.environ[k] = "1"
+    try:
+        with mp.get_context("spawn").Pool(procs) as pool:
+            # each worker cycles over its robots until its time budget is spent
+            res = pool.map(_cpu_worker, [(bt, N, budget_s, list(range(w, B, procs)) * 1000)
+                                         for w in range(procs)])
+    finally:
+        for k, v in env_keep.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    done = sum(r[1] for r in res)
+    dt = max(r[2] for r in res)
+    return done / dt, done, dt, procs
 
 
 def time_callers(eng, h, B, N, dev, stream, reps=20):
@@ -146,10 +192,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    # one rank per GPU; ranks beyond the visible devices wrap around (only a rehearsal
+    # of the N > 1 path on a smaller box does that).  MPCQP_BENCH_BACKEND=gloo is for
+    # such rehearsals too: the measured path is "nccl" (RCCL over xGMI).
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("MPCQP_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from mpcqp import LinearMpc
     from mpcqp.dist import gather_u0
@@ -204,7 +258,8 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in events]
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    tmax = torch.tensor([elapsed], dtype=torch.float64,
+                        device=dev if world == 1 or dist.get_backend() == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     elapsed = float(tmax.item())
@@ -240,14 +295,22 @@ def main():
 
     callers = None if args.no_callers else time_callers(eng, host[0], Bpg, N, dev, stream)
 
+    gather_label = ""
+    if world > 1 and not args.no_gather:
+        be = dist.get_backend()
+        gather_label = " + " + ("RCCL" if be == "nccl" else be) + " all-gather of u0"
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu:
-            v, done, dt = cpu_baseline(host[0], N, args.cpu_seconds)
-            cpu = {"value": v, "unit": "QP/s", "cores": 1, "kind": "port",
-                   "sample": f"{done} robots of the config's first synthetic batch in {dt:.1f}s: "
-                             "reference-faithful NumPy formulation (oracle/formulation.py) + "
-                             "exact float64 dual active-set QP (oracle/qp.py), 1 thread"}
+            v1, done1, dt1 = cpu_baseline(host[0], N, args.cpu_seconds)
+            vm, donem, dtm, procs = cpu_baseline_all_cores(host[0], N, args.cpu_seconds / 2)
+            cpu = {"value": vm, "unit": "QP/s", "cores": procs, "kind": "port",
+                   "sample": f"{donem} robot solves (the config's first synthetic batch, cycled) in {dtm:.1f}s on "
+                             f"{procs} processes x 1 thread ({_cpu_model()}): reference-faithful NumPy "
+                             "formulation (oracle/formulation.py) + exact float64 dual active-set QP "
+                             "(oracle/qp.py)",
+                   "single_core": {"value": v1, "cores": 1,
+                                   "sample": f"{done1} robots in {dt1:.1f}s, 1 process x 1 thread"}}
         line = {
             "metric": "QP solves/sec (whole node), horizon=10 GRF QP, at 1/2/4/8 MI355X",
             "value": qps,
@@ -264,8 +327,7 @@ def main():
             "config": {"workload": f"{args.config}: batch {Bpg}/GPU, horizon {N}, gaits {'+'.join(gaits)}, "
                                    f"robots {'+'.join(robots)}" + (f", cone tilt <= {tilt} deg" if tilt else ""),
                        "batch_per_gpu": Bpg, "horizon": N, "global_batch": world * Bpg,
-                       "parallelism": f"robot-sharded x{world}" + ("" if world == 1 or args.no_gather
-                                                                   else " + RCCL all-gather of u0")},
+                       "parallelism": f"robot-sharded x{world}" + gather_label},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP64_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic},
             "cpu_baseline": cpu,

@@ -26,6 +26,8 @@ def gather_u0(u0_local, total=None, group=None):
     world = dist.get_world_size(group)
     if world == 1:
         return u0_local
+    if u0_local.is_cuda and dist.get_backend(group) == "gloo":   # gloo is a host backend
+        return gather_u0(u0_local.cpu(), total, group).to(u0_local.device)
     b = u0_local.shape[0]
     if total is None:
         counts = [b] * world
