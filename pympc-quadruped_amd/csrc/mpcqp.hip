@@ -230,6 +230,11 @@ __device__ __forceinline__ int wave_argmin_d(double v, double& vmin_out) {
   if (__popcll(cand) == 1) {
     l = uni(__builtin_ctzll(cand));
     vmin_out = readlane_d(v, l);
+  } else if (fm == INFINITY && __ballot(v < INFINITY) == 0ull) {
+    // no candidate in any lane (e.g. no active slot blocks the step): the common
+    // all-+inf tie needs no f64 reduction
+    l = 0;
+    vmin_out = INFINITY;
   } else {
     const double vv = (f == fm) ? v : INFINITY;
     const double m = wave_min(vv);
