@@ -223,14 +223,18 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   };
   // drop-path variant: column descriptors re-read per entry (no extra live registers)
   auto hrow_slow = [&](int r, double (&h)[8]) {
-    const int row = 4 * tr + r;
+    // tc / tr made opaque: the descriptors are recomputed here rather than kept
+    // live (spilled) from the H build across the whole solve
+    int tco = tc, tro = tr;
+    asm volatile("" : "+v"(tco), "+v"(tro));
+    const int row = 4 * tro + r;
     const int sa = row < n ? row / 3 : 0;
     const int ja = sm.mt.foot_t[sa];
     const int car = 3 * sm.mt.foot_leg[sa] + row % 3;
     const double r2 = smfy.rd2[row < n ? car : 0];
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-      const int col = 8 * tc + c;
+      const int col = 8 * tco + c;
       const int sb = col < n ? col / 3 : 0;
       const double hv = form_h(smfy, N, ja, car, sm.mt.foot_t[sb], 3 * sm.mt.foot_leg[sb] + col % 3) +
                         (row == col ? r2 : 0.0);
@@ -357,7 +361,8 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   // opposite t1 rows and never enters (s = +inf): it only adds degenerate steps
   // at the cone apex.  Neither choice changes the (unique) optimum.
   int cz[CPL], crt[CPL];
-  double s[CPL], rn[CPL];
+  double s[CPL];
+  float rn[CPL];   // 1 / sqrt(a_c^T W a_c): only scales the f32-preselected row key
   auto cdot = [&](const double* v, int k) -> double {
     const double* a = sm.mt.rows[crt[k]];
     const double* vf = v + cz[k];
@@ -379,7 +384,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     double q = 0.0;
 #pragma unroll
     for (int i = 0; i < 3; ++i) q = fma(a[i], fma(w[3 * i], a[0], fma(w[3 * i + 1], a[1], w[3 * i + 2] * a[2])), q);
-    rn[k] = ok && q > 0.0 ? __builtin_amdgcn_rsq(q) : 1.0;
+    rn[k] = ok && q > 0.0 ? (float)__builtin_amdgcn_rsq(q) : 1.0f;
   }
   double x[VPL], u[VPL];
 #pragma unroll
@@ -421,7 +426,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       // most violated row in the dual metric (f32-rounded keys, lowest lane on ties)
       double key[CPL];
 #pragma unroll
-      for (int k = 0; k < CPL; ++k) key[k] = s[k] < -tol ? s[k] * rn[k] : INFINITY;
+      for (int k = 0; k < CPL; ++k) key[k] = s[k] < -tol ? s[k] * (double)rn[k] : INFINITY;
       double bv = key[0];
       int bk = 0;
 #pragma unroll
