@@ -151,3 +151,27 @@ def test_full_size_properties():
         for b in range(0, B, B // 8):
             x, _, _ = oracle_solution(bt, b, N)
             assert rel_err_u0(u0[b], x[:12]) < TOL_U0, (N, b)
+
+
+@pytest.mark.parametrize("N", [10, 16])
+def test_binding_bounds_and_friction_extremes(N):
+    """Per-robot cone parameters at their extremes, in both capacity classes: a
+    40 N fz_max (the fz <= ub row binds on 4-10 foot-steps, mpc.py:253-257), low
+    and high friction (mu = 0.2 / 1.5, mpc.py:239-245) and a 4x heavier body."""
+    from mpcqp.synthetic import make_batch
+    bt = make_batch(8, N, seed=31, gaits=("trot10", "pace10", "bound8"), robots=("a1",))
+    bt["robot"][0:2, 8] = 40.0
+    bt["robot"][2:4, 7] = 0.2
+    bt["robot"][4:6, 7] = 1.5
+    bt["robot"][6:8, 0] *= 4.0
+    u0, U, status, _ = _solve(_engine(N), bt)
+    assert (status == 0).all(), status
+    bound_rows = 0
+    for b in range(8):
+        x, _, _ = oracle_solution(bt, b, N)
+        assert rel_err_u0(u0[b], x[:12]) < TOL_U0, (b, u0[b], x[:12])
+        assert rel_err_u0(U[b], x) < TOL_U0, b
+        fz = U[b].reshape(-1, 3)[:, 2]
+        assert np.all(fz <= bt["robot"][b, 8] * (1 + 1e-5))
+        bound_rows += int(np.sum(np.abs(x.reshape(-1, 3)[:, 2] - bt["robot"][b, 8]) < 1e-6))
+    assert bound_rows >= 8   # the case really exercises the upper-bound rows
