@@ -217,11 +217,11 @@ def main():
     nbat = 4
     host = [make_batch(Bpg, N, seed=1000 * (k + 1) + rank, gaits=gaits, robots=robots, tilt_deg=tilt)
             for k in range(nbat)]
-    # the caller knows its contact schedules: promise the largest stance count so a
-    # workload that fits the 64-variable class launches only that kernel
+    # the caller knows its contact schedules: promise the largest stance count so the
+    # engine launches only the capacity classes the workload can reach
     max_stance = int(max((h["contact"] > 0).reshape(Bpg, -1).sum(1).max() for h in host))
     eng = LinearMpc(horizon=N, robot=robots[0], device=dev, max_iter=args.max_iter,
-                    max_stance=max_stance if 3 * max_stance <= 64 else 0)
+                    max_stance=max_stance)
     dev_b = []
     for h in host:
         dev_b.append({k: torch.as_tensor(v).to(dev).contiguous() for k, v in h.items()})

@@ -11,6 +11,8 @@
 //
 // ONE WORKGROUP PER ROBOT, nothing but the inputs and outputs touches HBM:
 //   class NV =  64: 2 waves, n = 3 * #stance <= 64   (mpcqp_kernel_64)
+//   class NV =  96: 6 waves, 4 x 6 tiles, n <= 96   (mpcqp_kernel_96, fed by a
+//                   device queue the first class fills)
 //   class NV = 128: 8 waves, n <= 126                (mpcqp_kernel_128, fed by a
 //                   device queue the first class fills)
 // Formulation in closed form (mpcqp_form.h); H^-1 by a symmetric sweep over
@@ -195,6 +197,23 @@ __device__ __forceinline__ void st8(double* base, int k, const double (&v)[8]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) p[i] = d2{v[2 * i], v[2 * i + 1]};
 }
+// TW consecutive doubles starting at element TW k (TW even; 16-B aligned LDS vectors)
+template <int TW>
+__device__ __forceinline__ void ldt(double (&v)[TW], const double* base, int k) {
+  const d2* p = reinterpret_cast<const d2*>(base + TW * k);
+#pragma unroll
+  for (int i = 0; i < TW / 2; ++i) {
+    const d2 x = p[i];
+    v[2 * i] = x[0];
+    v[2 * i + 1] = x[1];
+  }
+}
+template <int TW>
+__device__ __forceinline__ void stt(double* base, int k, const double (&v)[TW]) {
+  d2* p = reinterpret_cast<d2*>(base + TW * k);
+#pragma unroll
+  for (int i = 0; i < TW / 2; ++i) p[i] = d2{v[2 * i], v[2 * i + 1]};
+}
 __device__ __forceinline__ void ld4(double (&v)[4], const double* base, int k) {
   const d2* p = reinterpret_cast<const d2*>(base + 4 * k);
   const d2 a = p[0], b = p[1];
@@ -260,16 +279,42 @@ __device__ __forceinline__ int wave_argmin_f32(double v, double& vmin_out) {
 #include "mpcqp_plan.h"
 
 // Class NV = 64: one 2-wave workgroup per robot of the batch.  Robots with more
-// than 64 stance variables are appended to `queue` (when given) for class 128.
+// than 64 stance variables are appended to `queue` (when given) for class 96, those
+// with more than 96 to `queue_big` (when given) for class 128.
 __global__ __launch_bounds__(Cfg<64>::NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void mpcqp_kernel_64(
     KParams P, int B, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
-    int* __restrict__ queue) {
+    int* __restrict__ queue, int* __restrict__ queue_big) {
   __shared__ SharedT<64> sm;
   const int b = blockIdx.x;
   if (b >= B) return;
-  solve_robot<64>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, queue);
+  solve_robot<64>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, queue, queue_big);
+}
+
+// Class NV = 96: one 6-wave workgroup (4 x 6 register tiles) per robot queued by
+// class 64 (64 < n <= 96: the N = 16 trot / pace / bound schedules); robots with more
+// stance variables go on to class 128 through `qout`.  Same launch / reset protocol
+// as class 128 below.
+__global__ __launch_bounds__(Cfg<96>::NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void mpcqp_kernel_96(
+    KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
+    const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
+    float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
+    int* __restrict__ queue, int* __restrict__ qout) {
+  __shared__ SharedT<96> sm;
+  const int tid = threadIdx.x;
+  const int k = blockIdx.x;
+  const int cnt = uni(__hip_atomic_load(&queue[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (k < cnt) {
+    const int b = uni(queue[4 + k]);
+    solve_robot<96>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, qout);
+  }
+  if (tid == 0) {
+    if (atomicAdd(&queue[2], 1) == (int)gridDim.x - 1) {
+      atomicExch(&queue[0], 0);
+      atomicExch(&queue[2], 0);
+    }
+  }
 }
 
 // Class NV = 128: one 8-wave workgroup per queued robot.  The launch has one
@@ -308,7 +353,8 @@ struct mpcqp_ctx {
   int stance_hint;
   int ncu;
   int qcap;           // robots the device queue can hold
-  int* queue;         // [count, next, finished, pad, robots...] for class 128
+  int* queue;         // two queues of [count, next, finished, pad, robots... (qcap)]:
+                      // class 64 -> class 96, class 96 -> class 128
   double dt_control;  // planner constants (mpcqp_set_planner)
   double gravity;
   double max_pos_error;
@@ -382,29 +428,38 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   for (int i = 0; i < NX; ++i) kp.q[i] = ctx->params.q_diag[i];
   for (int i = 0; i < NU; ++i) kp.r[i] = ctx->params.r_diag[i];
   hipStream_t st = (hipStream_t)stream;
-  // robots with more than 64 stance variables are queued for class 128, unless
-  // the caller promised (stance hint) that none exceeds class 64
+  // robots with more than 64 stance variables are queued for class 96, those with
+  // more than 96 on for class 128 -- unless the caller promised (stance hint) that
+  // none exceeds the smaller class
   const bool large = !(ctx->stance_hint > 0 && 3 * ctx->stance_hint <= 64);
+  const bool huge = large && !(ctx->stance_hint > 0 && 3 * ctx->stance_hint <= 96);
   if (large && batch > ctx->qcap) {
     if (ctx->queue) (void)hipFree(ctx->queue);
     ctx->queue = nullptr;
     ctx->qcap = 0;
-    if (hipMalloc(&ctx->queue, sizeof(int) * (4 + (size_t)batch)) != hipSuccess)
+    if (hipMalloc(&ctx->queue, sizeof(int) * 2 * (4 + (size_t)batch)) != hipSuccess)
       return set_err(ctx, MPCQP_ERR_ALLOC, "queue allocation failed");
-    if (hipMemset(ctx->queue, 0, sizeof(int) * 4) != hipSuccess)
+    if (hipMemset(ctx->queue, 0, sizeof(int) * 2 * (4 + (size_t)batch)) != hipSuccess)
       return set_err(ctx, MPCQP_ERR_HIP, "queue init failed");
     ctx->qcap = batch;
   }
   int* q = large ? ctx->queue : nullptr;
+  int* q2 = huge ? ctx->queue + 4 + ctx->qcap : nullptr;
   hipLaunchKernelGGL(mpcqp_kernel_64, dim3(batch), dim3(Cfg<64>::NT), 0, st, kp, (int)batch, x0, xref, contact,
-                     feet, robot, u0, U, (int*)status, (int*)iters, q);
+                     feet, robot, u0, U, (int*)status, (int*)iters, q, q2);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch: ") + hipGetErrorString(e));
   if (large) {
-    hipLaunchKernelGGL(mpcqp_kernel_128, dim3(batch), dim3(Cfg<128>::NT), 0, st, kp, x0, xref, contact, feet, robot,
-                       u0, U, (int*)status, (int*)iters, q);
+    hipLaunchKernelGGL(mpcqp_kernel_96, dim3(batch), dim3(Cfg<96>::NT), 0, st, kp, x0, xref, contact, feet, robot,
+                       u0, U, (int*)status, (int*)iters, q, q2);
     e = hipGetLastError();
-    if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (large): ") + hipGetErrorString(e));
+    if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (96): ") + hipGetErrorString(e));
+  }
+  if (huge) {
+    hipLaunchKernelGGL(mpcqp_kernel_128, dim3(batch), dim3(Cfg<128>::NT), 0, st, kp, x0, xref, contact, feet, robot,
+                       u0, U, (int*)status, (int*)iters, q2);
+    e = hipGetLastError();
+    if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (128): ") + hipGetErrorString(e));
   }
   return MPCQP_OK;
 }

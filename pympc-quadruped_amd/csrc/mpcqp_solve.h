@@ -3,9 +3,12 @@
 //
 // Capacity class NV (stance variables n = 3 * #stance <= NV):
 //   NV =  64: 2 waves (128 threads) per robot -- every trot/pace/bound schedule at N <= 10
-//   NV = 128: 8 waves (512 threads) per robot -- N = 16/20 schedules, standing at N <= 10
+//   NV =  96: 6 waves (384 threads) per robot -- N = 16 schedules (n <= 96)
+//   NV = 128: 8 waves (512 threads) per robot -- N = 20 schedules, standing at N <= 10
 // Register tiles: lane t = (tr, tc) = (t / TCN, t % TCN) holds rows 4tr..4tr+3 and
-// columns 8tc..8tc+7 of each NV x NV matrix (32 doubles per matrix per lane).
+// columns TW tc..TW tc+TW-1 of each NV x NV matrix (TW = 8: 32 doubles per matrix
+// per lane; class 96 uses TW = 6 -- 24 doubles, and a foot-step's 3 columns never
+// straddle two tiles).
 //
 // Solver: Goldfarb-Idnani dual active set (Math. Prog. 27, 1983) on
 //   min 1/2 x^T H x + g^T x   s.t.  a_c . x >= b_c  (6 one-sided cone rows per foot-step)
@@ -24,13 +27,16 @@
 
 template <int NV>
 struct Cfg {
-  static constexpr int NW = NV * NV / 2048;   // waves per robot
+  static constexpr int TW = NV == 96 ? 6 : 8;   // tile width: 4 x TW register tiles
+  static constexpr int NW = NV * NV / (4 * TW * LANES);   // waves per robot
   static constexpr int NT = NW * LANES;
-  static constexpr int TCN = NV / 8;          // tile columns (lanes per tile row)
+  static constexpr int TCN = NV / TW;         // tile columns (lanes per tile row)
   static constexpr int RPW = 256 / TCN;       // tile rows (slots / variables) per wave
   static constexpr int CPL = NV / 32;         // constraint rows per lane (m = 6S <= 2NV)
-  static constexpr int VPL = NV / 64;         // variables / slots per lane
-  static_assert(NW * LANES * 32 == NV * NV, "4 x 8 tiles");
+  static constexpr int VPL = (NV + LANES - 1) / LANES;   // variables / slots per lane
+  static constexpr int VEC = VPL * LANES;     // LDS vector length (entries >= NV are padding)
+  static_assert(NW * LANES * 4 * TW == NV * NV, "4 x TW tiles");
+  static_assert(TCN == 8 || TCN == 16, "tile rows are reduced over 8 or 16 lanes");
 };
 
 // Class 64 keeps a copy of H (its register tiles, lane-interleaved) in LDS for the
@@ -57,23 +63,23 @@ struct alignas(16) SharedT {
   RobotMeta mt;
   union {
     struct {
-      alignas(16) double zc[2][NV];   // sweep pivot column (double-buffered); in the loop:
+      alignas(16) double zc[2][Cfg<NV>::VEC];   // sweep pivot column (double-buffered); in the loop:
                                       // z2 = P a_p2 of a pair step (double-buffered)
-      alignas(16) double vz[2][NV];   // z = P a_p (double-buffered by iteration)
+      alignas(16) double vz[2][Cfg<NV>::VEC];   // z = P a_p (double-buffered by iteration)
     };
-    double wb[4 * NV];   // between sweep and loop: W's 3x3 foot-step blocks (9 S <= 4 NV)
+    double wb[4 * Cfg<NV>::VEC];   // between sweep and loop: W's 3x3 foot-step blocks (9 S <= 4 NV)
   };
-  alignas(16) double vr[2][NV];   // r = R a_p (slot-indexed)
+  alignas(16) double vr[2][Cfg<NV>::VEC];   // r = R a_p (slot-indexed)
   union {
     struct {
-      alignas(16) double vx[NV];  // x (before and after the loop)
-      alignas(16) double gv[NV];  // g (before the loop)
+      alignas(16) double vx[Cfg<NV>::VEC];  // x (before and after the loop)
+      alignas(16) double gv[Cfg<NV>::VEC];  // g (before the loop)
     };
-    alignas(16) double vr2[2][NV];   // in the loop: r2 = R a_p2 of a pair step
+    alignas(16) double vr2[2][Cfg<NV>::VEC];   // in the loop: r2 = R a_p2 of a pair step
   };
-  alignas(16) double rl[NV];      // drop path: R_l, H R_l^T, R H R_l^T
-  alignas(16) double tv[NV];
-  alignas(16) double yv[NV];
+  alignas(16) double rl[Cfg<NV>::VEC];      // drop path: R_l, H R_l^T, R H R_l^T
+  alignas(16) double tv[Cfg<NV>::VEC];
+  alignas(16) double yv[Cfg<NV>::VEC];
   double wmax[Cfg<NV>::NW];
 };
 
@@ -112,16 +118,16 @@ template <int TCN>
 __device__ __forceinline__ bool twriter(int lane) { return TCN == 16 ? (lane & 9) == 0 : (lane & 1) == 0; }
 
 // y = M v, v in LDS; returns row trow(tr, lane)'s value
-template <int TCN>
-__device__ __forceinline__ double tile_matvec4(const double (&M)[4][8], const double* v, int tc, int lane) {
-  double vs[8];
-  ld8(vs, v, tc);
+template <int TCN, int TW>
+__device__ __forceinline__ double tile_matvec4(const double (&M)[4][TW], const double* v, int tc, int lane) {
+  double vs[TW];
+  ldt<TW>(vs, v, tc);
   double acc[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     double a = 0.0, b2 = 0.0;
 #pragma unroll
-    for (int c = 0; c < 8; c += 2) {
+    for (int c = 0; c < TW; c += 2) {
       a = fma(M[r][c], vs[c], a);
       b2 = fma(M[r][c + 1], vs[c + 1], b2);
     }
@@ -132,14 +138,14 @@ __device__ __forceinline__ double tile_matvec4(const double (&M)[4][8], const do
 
 // z / r column combination: out[r] = sum_k al_k M[r][(C0 + k) & 7]; the R half
 // only where the wave's slot rows hold an active constraint (rlive, wave-uniform)
-template <int C0>
-__device__ __forceinline__ void colcombo(const double (&Pm)[4][8], const double (&Rm)[4][8], int tc, int tcA,
+template <int C0, int TW>
+__device__ __forceinline__ void colcombo(const double (&Pm)[4][TW], const double (&Rm)[4][TW], int tc, int tcA,
                                          double a0, double a1, double a2, bool rlive, double (&zq)[4],
                                          double (&rq)[4]) {
-  const double al0 = (tc == tcA + ((C0 + 0) >> 3)) ? a0 : 0.0;
-  const double al1 = (tc == tcA + ((C0 + 1) >> 3)) ? a1 : 0.0;
-  const double al2 = (tc == tcA + ((C0 + 2) >> 3)) ? a2 : 0.0;
-  constexpr int c0 = C0 & 7, c1 = (C0 + 1) & 7, c2 = (C0 + 2) & 7;
+  const double al0 = (tc == tcA + (C0 + 0) / TW) ? a0 : 0.0;
+  const double al1 = (tc == tcA + (C0 + 1) / TW) ? a1 : 0.0;
+  const double al2 = (tc == tcA + (C0 + 2) / TW) ? a2 : 0.0;
+  constexpr int c0 = C0 % TW, c1 = (C0 + 1) % TW, c2 = (C0 + 2) % TW;
 #pragma unroll
   for (int r = 0; r < 4; ++r) zq[r] = fma(al2, Pm[r][c2], fma(al1, Pm[r][c1], al0 * Pm[r][c0]));
   if (rlive) {
@@ -164,15 +170,17 @@ __device__ __forceinline__ void write_empty_t(int b, int tid, int N, int code, f
 }
 
 // One robot.  A robot exceeding NV is appended to `queue` (when given) for the
-// next capacity class, otherwise reported MPCQP_STATUS_TOO_LARGE.
+// next capacity class -- or to `queue_big` for the one after, when it exceeds
+// that too -- otherwise reported MPCQP_STATUS_TOO_LARGE.
 template <int NV>
 __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>& sm, const float* __restrict__ x0g,
                                             const float* __restrict__ xrefg, const float* __restrict__ contactg,
                                             const float* __restrict__ feetg, const float* __restrict__ robotg,
                                             float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg,
-                                            int* __restrict__ itersg, int* __restrict__ queue) {
+                                            int* __restrict__ itersg, int* __restrict__ queue,
+                                            int* __restrict__ queue_big = nullptr) {
   using C = Cfg<NV>;
-  constexpr int NT = C::NT, TCN = C::TCN, CPL = C::CPL, VPL = C::VPL, RPW = C::RPW;
+  constexpr int NT = C::NT, TCN = C::TCN, CPL = C::CPL, VPL = C::VPL, RPW = C::RPW, TW = C::TW;
   const int tid = threadIdx.x;
   const int lane = tid & (LANES - 1), wave = uni(tid >> 6);
   const int tr = tid / TCN, tc = tid % TCN;
@@ -196,8 +204,11 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   const int S = uni(sm.mt.S);
   const int n = 3 * S, m = 6 * S;
   if (n > NV) {
-    if (queue) {   // the next capacity class takes it
-      if (tid == 0) queue[4 + atomicAdd(&queue[0], 1)] = b;
+    // the next capacity class takes it: `queue`, or `queue_big` (when given) for a
+    // robot beyond class 96 as well
+    int* const qn = (queue_big && n > 96) ? queue_big : queue;
+    if (qn) {
+      if (tid == 0) qn[4 + atomicAdd(&qn[0], 1)] = b;
       return;
     }
     write_empty_t<NT>(b, tid, N, MPCQP_STATUS_TOO_LARGE, u0g, Ug, statusg, itersg);
@@ -212,17 +223,17 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 
   // row `r` of the lane's H tile (identity padding beyond n); cj / cc: the tile
   // columns' foot-step horizon step and input column
-  auto hcols = [&](int (&cj)[8], int (&cc)[8]) {
+  auto hcols = [&](int (&cj)[TW], int (&cc)[TW]) {
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const int col = 8 * tc + c;
+    for (int c = 0; c < TW; ++c) {
+      const int col = TW * tc + c;
       const int sb = col < n ? col / 3 : 0;
       cj[c] = sm.mt.foot_t[sb];
       cc[c] = 3 * sm.mt.foot_leg[sb] + col % 3;
     }
   };
   // drop-path variant: column descriptors re-read per entry (no extra live registers)
-  auto hrow_slow = [&](int r, double (&h)[8]) {
+  auto hrow_slow = [&](int r, double (&h)[TW]) {
     // tc / tr made opaque: the descriptors are recomputed here rather than kept
     // live (spilled) from the H build across the whole solve
     int tco = tc, tro = tr;
@@ -233,30 +244,30 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     const int car = 3 * sm.mt.foot_leg[sa] + row % 3;
     const double r2 = smfy.rd2[row < n ? car : 0];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const int col = 8 * tco + c;
+    for (int c = 0; c < TW; ++c) {
+      const int col = TW * tco + c;
       const int sb = col < n ? col / 3 : 0;
       const double hv = form_h(smfy, N, ja, car, sm.mt.foot_t[sb], 3 * sm.mt.foot_leg[sb] + col % 3) +
                         (row == col ? r2 : 0.0);
       h[c] = (row < n && col < n) ? hv : (row == col ? 1.0 : 0.0);
     }
   };
-  auto hrow = [&](int r, const int (&cj)[8], const int (&cc)[8], double (&h)[8]) {
+  auto hrow = [&](int r, const int (&cj)[TW], const int (&cc)[TW], double (&h)[TW]) {
     const int row = 4 * tr + r;
     const int sa = row < n ? row / 3 : 0;
     const int ja = sm.mt.foot_t[sa];
     const int car = 3 * sm.mt.foot_leg[sa] + row % 3;
     const double r2 = smfy.rd2[row < n ? car : 0];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const int col = 8 * tc + c;
+    for (int c = 0; c < TW; ++c) {
+      const int col = TW * tc + c;
       const double hv = form_h(smfy, N, ja, car, cj[c], cc[c]) + (row == col ? r2 : 0.0);
       h[c] = (row < n && col < n) ? hv : (row == col ? 1.0 : 0.0);
     }
   };
-  double W[4][8];
+  double W[4][TW];
   {
-    int cj[8], cc[8];
+    int cj[TW], cc[TW];
     hcols(cj, cc);
 #pragma unroll
     for (int r = 0; r < 4; ++r) hrow(r, cj, cc, W[r]);   // unrolled: rows land in their registers
@@ -266,7 +277,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int c = 0; c < 8; ++c) sm.ht[(8 * r + c) * NT + tid] = W[r][c];
+      for (int c = 0; c < TW; ++c) sm.ht[(TW * r + c) * NT + tid] = W[r][c];
   }
   STAMP(2);
 
@@ -277,12 +288,13 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   // column and diagonal by masked FMAs -- no per-element selects.  KC compile-time
   // (register column), KT a runtime loop so the code stays in the instruction cache.
 #pragma unroll 1
-  for (int KT = 0; 8 * KT < n; ++KT) {
-    static_for<8>([&](auto KCc) {
+  for (int KT = 0; TW * KT < n; ++KT) {
+    static_for<TW>([&](auto KCc) {
       constexpr int KC = decltype(KCc)::value;
-      constexpr int KRR = KC & 3;
-      const int K = 8 * KT + KC;
-      const int KR = 2 * KT + (KC >> 2);
+      const int K = TW * KT + KC;
+      // pivot row K: tile row KR, register row KRR (compile-time when TW = 8)
+      const int KR = TW == 8 ? 2 * KT + (KC >> 2) : K >> 2;
+      const int KRR = TW == 8 ? (KC & 3) : (K & 3);
       if (K < n) {
         double* const zc = sm.zc[KC & 1];
         if (tc == KT) {
@@ -291,24 +303,34 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
           pz[1] = d2{W[2][KC], W[3][KC]};
         }
         fsync<NT>();
-        double zr[8], zi[4];
-        ld8(zr, zc, tc);
+        double zr[TW], zi[4];
+        ldt<TW>(zr, zc, tc);
         ld4(zi, zc, tr);
         const double inv = rcp_nr(zc[K]);
         double beta[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) beta[r] = -zi[r] * inv;
-        if (tr == KR) beta[KRR] = inv - 1.0;
+        if constexpr (TW == 8) {
+          if (tr == KR) beta[KC & 3] = inv - 1.0;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) beta[r] = (tr == KR && r == KRR) ? inv - 1.0 : beta[r];
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
-          for (int c = 0; c < 8; ++c) W[r][c] = fma(beta[r], zr[c], W[r][c]);
+          for (int c = 0; c < TW; ++c) W[r][c] = fma(beta[r], zr[c], W[r][c]);
         // column K: the pass left z_i - z_i d/d ~ 0 there; add z_i / d.  Diagonal:
         // d/d + 1 -> -1/d.
         const double cm = (tc == KT) ? inv : 0.0;
 #pragma unroll
         for (int r = 0; r < 4; ++r) W[r][KC] = fma(zi[r], cm, W[r][KC]);
-        W[KRR][KC] += (tc == KT && tr == KR) ? -inv - 2.0 : 0.0;
+        if constexpr (TW == 8) {
+          W[KC & 3][KC] += (tc == KT && tr == KR) ? -inv - 2.0 : 0.0;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) W[r][KC] += (tc == KT && tr == KR && r == KRR) ? -inv - 2.0 : 0.0;
+        }
       }
     });
   }
@@ -317,16 +339,24 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int c = 0; c < 8; ++c) W[r][c] = -W[r][c];
-  if (tc == (tr >> 1)) {
-    // diagonal entries: column r (even tile row) or 4 + r (odd); blended
-    // arithmetically -- a select between the two would index the tile at run time
-    const double odd = (double)(tr & 1);
+    for (int c = 0; c < TW; ++c) W[r][c] = -W[r][c];
+  if constexpr (TW == 8) {
+    if (tc == (tr >> 1)) {
+      // diagonal entries: column r (even tile row) or 4 + r (odd); blended
+      // arithmetically -- a select between the two would index the tile at run time
+      const double odd = (double)(tr & 1);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const double dv = fma(odd, W[r][4 + r], (1.0 - odd) * W[r][r]);
-      if (4 * tr + r < n) wd = fmax(wd, dv);
+      for (int r = 0; r < 4; ++r) {
+        const double dv = fma(odd, W[r][4 + r], (1.0 - odd) * W[r][r]);
+        if (4 * tr + r < n) wd = fmax(wd, dv);
+      }
     }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < TW; ++c)
+        if (4 * tr + r == TW * tc + c && 4 * tr + r < n) wd = fmax(wd, W[r][c]);
   }
   wd = wave_max_d(wd);
   if (lane == 0) sm.wmax[wave] = wd;
@@ -335,15 +365,15 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const int row = 4 * tr + r, col = 8 * tc + c;
+    for (int c = 0; c < TW; ++c) {
+      const int row = 4 * tr + r, col = TW * tc + c;
       if (row < n && col < n && row / 3 == col / 3) sm.wb[9 * (row / 3) + 3 * (row % 3) + col % 3] = W[r][c];
     }
   STAMP(3);
 
   // unconstrained minimiser x = -W g
   {
-    const double y = tile_matvec4<TCN>(W, sm.gv, tc, lane);
+    const double y = tile_matvec4<TCN, TW>(W, sm.gv, tc, lane);
     if (twriter<TCN>(lane)) sm.vx[trow(tr, lane)] = -y;
   }
   fsync<NT>();
@@ -396,11 +426,11 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   unsigned long long occ[VPL];
 #pragma unroll
   for (int k = 0; k < VPL; ++k) occ[k] = 0ull;
-  double Rm[4][8];
+  double Rm[4][TW];
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int c = 0; c < 8; ++c) Rm[r][c] = 0.0;
+    for (int c = 0; c < TW; ++c) Rm[r][c] = 0.0;
   auto slots_live = [&](int lo) -> bool {   // any occupied slot in [lo, lo + RPW)
     const unsigned long long w = occ[lo >> 6] >> (lo & 63);
     return (RPW >= 64 ? w : (w & ((1ull << RPW) - 1))) != 0ull;
@@ -449,8 +479,8 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       a2 = sgpr_d(sm.mt.rows[rp][2]);
       thr = sgpr_d(1e-12 * (a0 * a0 + a1 * a1 + a2 * a2) * wscale);
       v0 = 3 * (p / 6);
-      tcA = v0 >> 3;
-      c0 = v0 & 7;
+      tcA = v0 / TW;
+      c0 = v0 % TW;
       sp = sgpr_d(vmn);   // s_p, tracked like s[] (identical arithmetic)
       up = 0.0;
       // second candidate: the best row of any other foot-step
@@ -478,8 +508,8 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         b2 = sgpr_d(sm.mt.rows[rq][2]);
         thr2 = sgpr_d(1e-12 * (b0 * b0 + b1 * b1 + b2 * b2) * wscale);
         const int w0 = 3 * (p2 / 6);
-        tcA2 = w0 >> 3;
-        c02 = w0 & 7;
+        tcA2 = w0 / TW;
+        c02 = w0 % TW;
       }
       }
     }
@@ -495,17 +525,22 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     // 8 tA + cA, stored by the lanes of tile column tA
     auto combo_store = [&](int cA, int tA, double e0, double e1, double e2, double* dz, double* dr) {
       double zq[4], rq[4];
-      switch (cA) {
-        case 0: colcombo<0>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-        case 1: colcombo<1>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-        case 2: colcombo<2>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-        case 3: colcombo<3>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-        case 4: colcombo<4>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-        case 5: colcombo<5>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-        case 6: colcombo<6>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-        default: colcombo<7>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+      if constexpr (TW == 6) {   // foot-steps start at register column 0 or 3: never straddle
+        if (cA == 0) colcombo<0, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq);
+        else colcombo<3, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq);
+      } else {
+        switch (cA) {
+          case 0: colcombo<0, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+          case 1: colcombo<1, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+          case 2: colcombo<2, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+          case 3: colcombo<3, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+          case 4: colcombo<4, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+          case 5: colcombo<5, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+          case 6: colcombo<6, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+          default: colcombo<7, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+        }
       }
-      if (cA >= 6) {   // the foot-step straddles tile columns tA, tA + 1 (next lane)
+      if (TW == 8 && cA >= 6) {   // the foot-step straddles tile columns tA, tA + 1 (next lane)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           zq[r] += dpp_shl1(zq[r]);
@@ -608,9 +643,9 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         // rank-2 updates: row coefficients (al, be) = S^-1 (row's pair), then
         // M[r][c] -= al cz1[c] + be cz2[c]
         const double i11 = s22 * id, i12 = -s12 * id, i22 = zsp * id;
-        double cz1[8], cz2[8], z41[4], z42[4];
-        ld8(cz1, vz, tc);
-        ld8(cz2, vz2, tc);
+        double cz1[TW], cz2[TW], z41[4], z42[4];
+        ldt<TW>(cz1, vz, tc);
+        ldt<TW>(cz2, vz2, tc);
         ld4(z41, vz, tr);
         ld4(z42, vz2, tr);
 #pragma unroll
@@ -618,7 +653,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
           const double al = fma(i11, z41[r], i12 * z42[r]);
           const double be = fma(i12, z41[r], i22 * z42[r]);
 #pragma unroll
-          for (int c = 0; c < 8; ++c) W[r][c] = fma(-be, cz2[c], fma(-al, cz1[c], W[r][c]));
+          for (int c = 0; c < TW; ++c) W[r][c] = fma(-be, cz2[c], fma(-al, cz1[c], W[r][c]));
         }
         if (rlive || slots_live(RPW * wave)) {
           double r41[4], r42[4];
@@ -632,7 +667,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
             const double al = fma(i11, e1, i12 * e2);
             const double be = fma(i12, e1, i22 * e2);
 #pragma unroll
-            for (int c = 0; c < 8; ++c) Rm[r][c] = fma(-be, cz2[c], fma(-al, cz1[c], Rm[r][c]));
+            for (int c = 0; c < TW; ++c) Rm[r][c] = fma(-be, cz2[c], fma(-al, cz1[c], Rm[r][c]));
           }
         }
         p = -1;
@@ -677,7 +712,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     up = sgpr_d(up + tstep);
     SEC(add ? 5 : 6);
     // rank-1 updates  W += aW cv^T,  R += aR cv^T  (rows by the lane's tile row)
-    double aW[4], aR[4], cv[8];
+    double aW[4], aR[4], cv[TW];
     int zrow = -1;   // R row to clear (drop)
     if (add) {
       // slot q (first free); P -= z z^T / sigma ; R -= (r - e_q) z^T / sigma
@@ -688,7 +723,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       const double is = rcp_nr(zsp);
       double zr4[4], rr4[4];
       ld4(zr4, vz, tr);
-      ld8(cv, vz, tc);
+      ldt<TW>(cv, vz, tc);
       ld4(rr4, vr, tr);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -705,13 +740,13 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       // drop slot l: eta = Minv_ll, y = Minv[:, l] = R (H R_l^T)
       const int lt = l >> 2, lr = l & 3;
       if (tr == lt) {
-        double row[8];
+        double row[TW];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) row[c] = lr == 0 ? Rm[0][c] : lr == 1 ? Rm[1][c] : lr == 2 ? Rm[2][c] : Rm[3][c];
-        st8(sm.rl, tc, row);
+        for (int c = 0; c < TW; ++c) row[c] = lr == 0 ? Rm[0][c] : lr == 1 ? Rm[1][c] : lr == 2 ? Rm[2][c] : Rm[3][c];
+        stt<TW>(sm.rl, tc, row);
       }
       fsync<NT>();
-      ld8(cv, sm.rl, tc);
+      ldt<TW>(cv, sm.rl, tc);
       {
         double acc[4] = {0.0, 0.0, 0.0, 0.0};
         if constexpr (SharedT<NV>::kHStore) {   // the lane's H tile, from LDS
@@ -719,20 +754,20 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
           for (int r = 0; r < 4; ++r) {
             double a = 0.0, a2 = 0.0;
 #pragma unroll
-            for (int c = 0; c < 8; c += 2) {
-              a = fma(sm.ht[(8 * r + c) * NT + tid], cv[c], a);
-              a2 = fma(sm.ht[(8 * r + c + 1) * NT + tid], cv[c + 1], a2);
+            for (int c = 0; c < TW; c += 2) {
+              a = fma(sm.ht[(TW * r + c) * NT + tid], cv[c], a);
+              a2 = fma(sm.ht[(TW * r + c + 1) * NT + tid], cv[c + 1], a2);
             }
             acc[r] = a + a2;
           }
         } else {
 #pragma unroll 1
           for (int r = 0; r < 4; ++r) {
-            double h[8];
+            double h[TW];
             hrow_slow(r, h);
             double a = 0.0;
 #pragma unroll
-            for (int c = 0; c < 8; ++c) a = fma(h[c], cv[c], a);
+            for (int c = 0; c < TW; ++c) a = fma(h[c], cv[c], a);
             static_for<4>([&](auto Rr) {
               constexpr int rr = decltype(Rr)::value;
               acc[rr] = (rr == r) ? a : acc[rr];
@@ -744,7 +779,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       }
       fsync<NT>();
       {
-        const double yvv = tile_matvec4<TCN>(Rm, sm.tv, tc, lane);
+        const double yvv = tile_matvec4<TCN, TW>(Rm, sm.tv, tc, lane);
         if (twriter<TCN>(lane)) sm.yv[trow(tr, lane)] = yvv;
       }
       fsync<NT>();
@@ -765,18 +800,18 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int c = 0; c < 8; ++c) W[r][c] = fma(aW[r], cv[c], W[r][c]);
+      for (int c = 0; c < TW; ++c) W[r][c] = fma(aW[r], cv[c], W[r][c]);
     if (rlive || slots_live(RPW * wave)) {   // this wave's slot rows, before or after the step
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int c = 0; c < 8; ++c) Rm[r][c] = fma(aR[r], cv[c], Rm[r][c]);
+        for (int c = 0; c < TW; ++c) Rm[r][c] = fma(aR[r], cv[c], Rm[r][c]);
     }
     if (zrow >= 0) {
       if (tr == (zrow >> 2)) {   // clear row l of R exactly
         const int lr = zrow & 3;
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
+        for (int c = 0; c < TW; ++c) {
           if (lr == 0) Rm[0][c] = 0.0;
           if (lr == 1) Rm[1][c] = 0.0;
           if (lr == 2) Rm[2][c] = 0.0;
