@@ -308,9 +308,8 @@ __global__ __launch_bounds__(Cfg<96>::NT) __attribute__((amdgpu_waves_per_eu(2, 
   if (k < cnt) {
     const int b = uni(queue[4 + k]);
     solve_robot<96>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, qout);
-  }
-  if (tid == 0) {
-    if (atomicAdd(&queue[2], 1) == (int)gridDim.x - 1) {
+    // only the cnt workers count themselves (no contended atomic from the idle rest)
+    if (tid == 0 && atomicAdd(&queue[2], 1) == cnt - 1) {
       atomicExch(&queue[0], 0);
       atomicExch(&queue[2], 0);
     }
@@ -319,8 +318,8 @@ __global__ __launch_bounds__(Cfg<96>::NT) __attribute__((amdgpu_waves_per_eu(2, 
 
 // Class NV = 128: one 8-wave workgroup per queued robot.  The launch has one
 // workgroup per robot of the batch (the host cannot know the queue length without a
-// sync); the ones beyond the queue count exit at once.  The last workgroup to finish
-// resets the counters for the next launch (queue[0] = count, queue[2] = finished
+// sync); the ones beyond the queue count exit at once.  The last queued robot's
+// workgroup to finish resets the counters for the next launch (queue[0] = count, queue[2] = finished
 // workgroups, queue[4..] = robot indices).  Workloads that fit class 64 skip this
 // launch via mpcqp_set_stance_hint.
 __global__ __launch_bounds__(Cfg<128>::NT) void mpcqp_kernel_128(
@@ -335,9 +334,8 @@ __global__ __launch_bounds__(Cfg<128>::NT) void mpcqp_kernel_128(
   if (k < cnt) {
     const int b = uni(queue[4 + k]);
     solve_robot<128>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, nullptr);
-  }
-  if (tid == 0) {
-    if (atomicAdd(&queue[2], 1) == (int)gridDim.x - 1) {
+    // only the cnt workers count themselves (no contended atomic from the idle rest)
+    if (tid == 0 && atomicAdd(&queue[2], 1) == cnt - 1) {
       atomicExch(&queue[0], 0);
       atomicExch(&queue[2], 0);
     }
