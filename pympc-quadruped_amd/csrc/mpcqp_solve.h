@@ -479,8 +479,8 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       a2 = sgpr_d(sm.mt.rows[rp][2]);
       thr = sgpr_d(1e-12 * (a0 * a0 + a1 * a1 + a2 * a2) * wscale);
       v0 = 3 * (p / 6);
-      tcA = v0 / TW;
-      c0 = v0 % TW;
+      tcA = (int)((unsigned)v0 / TW);   // v0 >= 0: shifts for TW = 8
+      c0 = (int)((unsigned)v0 % TW);
       sp = sgpr_d(vmn);   // s_p, tracked like s[] (identical arithmetic)
       up = 0.0;
       // second candidate: the best row of any other foot-step
@@ -508,8 +508,8 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         b2 = sgpr_d(sm.mt.rows[rq][2]);
         thr2 = sgpr_d(1e-12 * (b0 * b0 + b1 * b1 + b2 * b2) * wscale);
         const int w0 = 3 * (p2 / 6);
-        tcA2 = w0 / TW;
-        c02 = w0 % TW;
+        tcA2 = (int)((unsigned)w0 / TW);   // v0 >= 0: shifts for TW = 8
+        c02 = (int)((unsigned)w0 % TW);
       }
       }
     }

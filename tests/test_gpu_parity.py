@@ -175,3 +175,31 @@ def test_binding_bounds_and_friction_extremes(N):
         assert np.all(fz <= bt["robot"][b, 8] * (1 + 1e-5))
         bound_rows += int(np.sum(np.abs(x.reshape(-1, 3)[:, 2] - bt["robot"][b, 8]) < 1e-6))
     assert bound_rows >= 8   # the case really exercises the upper-bound rows
+
+
+def test_capacity_class_routing():
+    """One N = 16 call reaching every capacity class: n = 96 (class 96), n = 114 and
+    126 (class 128), n = 60 (class 64) and standing n = 192 (MPCQP_STATUS_TOO_LARGE),
+    then twice more (the device queues reset themselves), and with a stance hint the
+    batch breaks (the promise is the caller's: the robot beyond it is reported)."""
+    from mpcqp.synthetic import make_batch
+    N = 16
+    bt = make_batch(8, N, seed=41, gaits=("trot10",), robots=("a1",))
+    bt["contact"][1, :3, :] = 1.0                  # 3 trot steps made full stance: n = 114
+    bt["contact"][2, :5, :] = 1.0                  # n = 126 (the class 128 maximum)
+    bt["contact"][3, 10:, :] = 0.0                 # n = 60
+    bt["contact"][4] = 1.0                         # standing: n = 192
+    ns = 3 * (bt["contact"] > 0).reshape(8, -1).sum(1)
+    assert ns[1] > 96 and ns[2] == 126 and ns[3] <= 64 and ns[4] > 126
+    eng = _engine(N)
+    for _ in range(3):
+        u0, U, status, _ = _solve(eng, bt)
+        assert status[4] == 3 and np.all(u0[4] == 0)
+        for b in (0, 1, 2, 3, 5):
+            assert status[b] == 0, (b, status)
+            x, _, _ = oracle_solution(bt, b, N)
+            assert rel_err_u0(U[b], x) < TOL_U0, b
+    hinted = _engine(N, max_stance=32)             # promises n <= 96: class 128 not launched
+    _, _, st, _ = _solve(hinted, bt)
+    assert st[1] == 3 and st[2] == 3 and st[4] == 3
+    assert all(st[b] == 0 for b in (0, 3, 5, 6, 7))
