@@ -39,10 +39,10 @@ struct Cfg {
   static_assert(TCN == 8 || TCN == 16, "tile rows are reduced over 8 or 16 lanes");
 };
 
-// Class 64 keeps a copy of H (its register tiles, lane-interleaved) in LDS for the
-// drop path, in the space of the formulation scratch, which is dead once H is
-// built: 32 KB, so that 4 robots still share a CU's 160 KB.  Class 128 has no room
-// and recomputes H entries from Ya / Yb instead.
+// Every class keeps a copy of H (its register tiles, lane-interleaved) in LDS for
+// the drop path, in the space of the formulation scratch, which is dead once H is
+// built: 32 KB for class 64 (4 robots still share a CU's 160 KB), 72 / 128 KB for
+// classes 96 / 128, which hold one robot per CU anyway (VGPR-bound).
 template <int NV>
 struct FormArea {
   Form f;
@@ -50,7 +50,6 @@ struct FormArea {
 };
 template <int NV>
 struct alignas(16) SharedT {
-  static constexpr bool kHStore = NV == 64;
 #ifdef MPCQP_NO_PAIR
   static constexpr bool kPair = false;
 #else
@@ -58,7 +57,7 @@ struct alignas(16) SharedT {
 #endif
   union {
     FormArea<NV> fa;
-    double ht[kHStore ? NV * NV : 1];   // element e of thread t at ht[e * NT + t]
+    double ht[NV * NV];   // element e of thread t at ht[e * NT + t]
   };
   RobotMeta mt;
   union {
@@ -232,26 +231,6 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       cc[c] = 3 * sm.mt.foot_leg[sb] + col % 3;
     }
   };
-  // drop-path variant: column descriptors re-read per entry (no extra live registers)
-  auto hrow_slow = [&](int r, double (&h)[TW]) {
-    // tc / tr made opaque: the descriptors are recomputed here rather than kept
-    // live (spilled) from the H build across the whole solve
-    int tco = tc, tro = tr;
-    asm volatile("" : "+v"(tco), "+v"(tro));
-    const int row = 4 * tro + r;
-    const int sa = row < n ? row / 3 : 0;
-    const int ja = sm.mt.foot_t[sa];
-    const int car = 3 * sm.mt.foot_leg[sa] + row % 3;
-    const double r2 = smfy.rd2[row < n ? car : 0];
-#pragma unroll
-    for (int c = 0; c < TW; ++c) {
-      const int col = TW * tco + c;
-      const int sb = col < n ? col / 3 : 0;
-      const double hv = form_h(smfy, N, ja, car, sm.mt.foot_t[sb], 3 * sm.mt.foot_leg[sb] + col % 3) +
-                        (row == col ? r2 : 0.0);
-      h[c] = (row < n && col < n) ? hv : (row == col ? 1.0 : 0.0);
-    }
-  };
   auto hrow = [&](int r, const int (&cj)[TW], const int (&cc)[TW], double (&h)[TW]) {
     const int row = 4 * tr + r;
     const int sa = row < n ? row / 3 : 0;
@@ -272,7 +251,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
     for (int r = 0; r < 4; ++r) hrow(r, cj, cc, W[r]);   // unrolled: rows land in their registers
   }
-  if constexpr (SharedT<NV>::kHStore) {
+  {
     fsync<NT>();   // every lane is done reading the formulation scratch H overwrites
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -749,30 +728,16 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       ldt<TW>(cv, sm.rl, tc);
       {
         double acc[4] = {0.0, 0.0, 0.0, 0.0};
-        if constexpr (SharedT<NV>::kHStore) {   // the lane's H tile, from LDS
+        // the lane's H tile, from LDS
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            double a = 0.0, a2 = 0.0;
+        for (int r = 0; r < 4; ++r) {
+          double a = 0.0, a2 = 0.0;
 #pragma unroll
-            for (int c = 0; c < TW; c += 2) {
-              a = fma(sm.ht[(TW * r + c) * NT + tid], cv[c], a);
-              a2 = fma(sm.ht[(TW * r + c + 1) * NT + tid], cv[c + 1], a2);
-            }
-            acc[r] = a + a2;
+          for (int c = 0; c < TW; c += 2) {
+            a = fma(sm.ht[(TW * r + c) * NT + tid], cv[c], a);
+            a2 = fma(sm.ht[(TW * r + c + 1) * NT + tid], cv[c + 1], a2);
           }
-        } else {
-#pragma unroll 1
-          for (int r = 0; r < 4; ++r) {
-            double h[TW];
-            hrow_slow(r, h);
-            double a = 0.0;
-#pragma unroll
-            for (int c = 0; c < TW; ++c) a = fma(h[c], cv[c], a);
-            static_for<4>([&](auto Rr) {
-              constexpr int rr = decltype(Rr)::value;
-              acc[rr] = (rr == r) ? a : acc[rr];
-            });
-          }
+          acc[r] = a + a2;
         }
         const double tvv = tile_reduce<TCN>(acc, lane);
         if (twriter<TCN>(lane)) sm.tv[trow(tr, lane)] = tvv;
