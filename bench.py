@@ -35,8 +35,8 @@ CONFIGS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="config2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="override batch per GPU")
     ap.add_argument("--no-gather", action="store_true", help="skip the end-of-step u0 gather")
