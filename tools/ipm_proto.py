@@ -1,0 +1,305 @@
+"""NumPy model of the large-class solver: a Mehrotra interior point on the
+uncondensed horizon, its Newton systems solved by a Riccati recursion in
+information (Woodbury) form, and an active-set polish that returns the exact
+optimum.  It designs and debugs the HIP kernel step by step (same recursions,
+same stopping rules).  Not test infrastructure, not product code.
+
+    python tools/ipm_proto.py            # golden cases + synthetic standing robots
+
+Problem (per robot, swing foot-steps eliminated):
+    min 1/2 sum_k x_{k+1}^T Qh x_{k+1} + qh_k^T x_{k+1} + 1/2 u_k^T Rh u_k
+    s.t. x_{k+1} = A x_k + B u_k,  G f_j >= h_j for every stance foot-step j,
+which is exactly 1/2 U^T H U + g^T U + const of mpc.py:211-235 (H = 2(Su^T Qbar Su
++ Rbar)), so its optimum is the Drake-branch QP's.
+
+Riccati in information form (stage k, P = P_{k+1}):
+    E = B Ri B^T (Ri = Rt^-1, Rt block-diagonal per leg), S = (I + P E)^-1 P,
+    P_k = Qh + A^T S A.
+The textbook form P - P B (Rt + B^T P B)^-1 B^T P loses ~4 digits here: B has a
+6-dimensional null space (internal forces between feet) where only Rh = 2e-5 acts.
+"""
+import itertools
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "pympc-quadruped_amd"), os.path.join(ROOT, "tests")]
+
+from oracle import formulation as F  # noqa: E402
+
+TAU = float(os.environ.get("TAU", "0.995"))           # fraction to the boundary
+POLISH_MU = float(os.environ.get("POLISH_MU", "1e-7"))  # polish once mu < this * scale
+MU_FLOOR = float(os.environ.get("MU_FLOOR", "1e-13"))   # centring target floor
+NREF = int(os.environ.get("NREF", "2"))                 # Newton refinements in the polish
+NCORR = int(os.environ.get("NCORR", "8"))               # active-set corrections per polish
+STAT_TOL = float(os.environ.get("STAT_TOL", "1e-10"))
+MAX_IT = int(os.environ.get("MAX_IT", "60"))
+
+
+def cone(mu, normal):
+    """Rows a_r of a_r . f >= b_r: 4 pyramid rows, n.f >= 0, -n.f >= -ub."""
+    nrm = np.asarray(normal, np.float64)
+    nn = np.linalg.norm(nrm)
+    nrm = nrm / nn if nn > 0 else np.array([0.0, 0.0, 1.0])
+    t1 = np.array([1.0, 0.0, 0.0]) - nrm[0] * nrm
+    t1 /= np.linalg.norm(t1)
+    t2 = np.cross(nrm, t1)
+    return np.array([t1 + mu * nrm, -t1 + mu * nrm, t2 + mu * nrm, -t2 + mu * nrm, nrm, -nrm])
+
+
+def gj_inverse(M):
+    """Gauss-Jordan inverse without pivoting (I + P E is similar to an SPD matrix)."""
+    M = M.copy()
+    for k in range(M.shape[0]):
+        inv = 1.0 / M[k, k]
+        col, row = M[:, k].copy(), M[k, :].copy()
+        M -= np.outer(col, row) * inv
+        M[k, :] = row * inv
+        M[:, k] = -col * inv
+        M[k, k] = inv
+    return M
+
+
+def solve(Ad, Bd, x0, xref, contact, N, mu, fz_max, normal, q_diag=F.Q_DIAG, r_diag=F.R_DIAG,
+          verbose=False):
+    A = np.asarray(Ad, np.float64)
+    B = np.asarray(Bd, np.float64)
+    x0 = np.asarray(x0, np.float64)
+    xr = np.asarray(xref, np.float64).reshape(N, 13)
+    ct = np.asarray(contact).reshape(N, 4)
+    Qh = 2.0 * np.asarray(q_diag, np.float64)
+    Rh = 2.0 * np.asarray(r_diag, np.float64)
+    qh = -Qh[None, :] * xr
+    rows = cone(mu, normal)
+    use = [0, 1, 2, 3, 5] if mu > 0 else [0, 1, 2, 3, 4, 5]
+    G = rows[use]
+    R = len(use)
+    feet = [(k, leg) for k in range(N) for leg in range(4) if ct[k, leg] > 0]
+    nf = len(feet)
+    h = np.zeros((nf, R))
+    for j, (k, leg) in enumerate(feet):
+        h[j, -1] = -ct[k, leg] * fz_max
+    stance = np.zeros((N, 4), bool)
+    for (k, leg) in feet:
+        stance[k, leg] = True
+    m_tot = nf * R
+    Bleg = np.stack([B[:, 3 * l:3 * l + 3] for l in range(4)])   # (4, 13, 3)
+
+    def fview(U):
+        return np.array([U[k, 3 * leg:3 * leg + 3] for (k, leg) in feet]).reshape(nf, 3)
+
+    def gt(w):
+        out = np.zeros((N, 12))
+        for j, (k, leg) in enumerate(feet):
+            out[k, 3 * leg:3 * leg + 3] += G.T @ w[j]
+        return out
+
+    def gradient(U):
+        """H U + g (stance coordinates) by a forward simulation and the adjoint."""
+        X = np.zeros((N + 1, 13))
+        X[0] = x0
+        for k in range(N):
+            X[k + 1] = A @ X[k] + B @ U[k]
+        gr = np.zeros((N, 12))
+        nu = np.zeros(13)
+        for k in range(N - 1, -1, -1):
+            nu = Qh * X[k + 1] + qh[k] + (A.T @ nu if k < N - 1 else 0.0)
+            gr[k] = Rh * U[k] + B.T @ nu
+        return gr * np.repeat(stance, 3, axis=1)
+
+    def factor(Bl, Ri):
+        """S_k = (I + P_{k+1} E_k)^-1 P_{k+1}; Bl (N,4,13,3), Ri (N,4,3,3)."""
+        S = np.zeros((N, 13, 13))
+        P = np.diag(Qh)
+        for k in range(N - 1, -1, -1):
+            E = sum(Bl[k, l] @ Ri[k, l] @ Bl[k, l].T for l in range(4))
+            S[k] = gj_inverse(np.eye(13) + P @ E) @ P
+            S[k] = 0.5 * (S[k] + S[k].T)
+            P = np.diag(Qh) + A.T @ S[k] @ A
+        return S
+
+    def lsolve(Bl, Ri, S, rhs):
+        """(H + per-leg Rt - Rh) d = rhs on the legs' subspaces (Bl already projected)."""
+        p = np.zeros(13)
+        Y = np.zeros((N, 4, 3))
+        for k in range(N - 1, -1, -1):
+            for l in range(4):
+                Y[k, l] = Ri[k, l] @ (-rhs[k, 3 * l:3 * l + 3] + Bl[k, l].T @ p)
+            By = sum(Bl[k, l] @ Y[k, l] for l in range(4))
+            if k > 0:
+                p = A.T @ (p - S[k] @ By)
+        d = np.zeros((N, 12))
+        dx = np.zeros(13)
+        for k in range(N):
+            By = sum(Bl[k, l] @ Y[k, l] for l in range(4))
+            w = S[k] @ (By - A @ dx)
+            for l in range(4):
+                d[k, 3 * l:3 * l + 3] = Ri[k, l] @ (Bl[k, l].T @ w) - Y[k, l]
+            dx = A @ dx + sum(Bl[k, l] @ d[k, 3 * l:3 * l + 3] for l in range(4))
+        return d
+
+    def ipm_blocks(D):
+        Bl = np.zeros((N, 4, 13, 3))
+        Ri = np.zeros((N, 4, 3, 3))
+        for k in range(N):
+            for l in range(4):
+                Ri[k, l] = np.eye(3)
+        for j, (k, l) in enumerate(feet):
+            Bl[k, l] = Bleg[l]
+            Ri[k, l] = np.linalg.inv(np.diag(Rh[3 * l:3 * l + 3]) + G.T @ (D[j][:, None] * G))
+        return Bl, Ri
+
+    def polish(act):
+        """Equality-constrained optimum on `act` (null-space per foot), KKT-verified."""
+        Bl = np.zeros((N, 4, 13, 3))
+        Ri = np.zeros((N, 4, 3, 3))
+        Pi = np.zeros((N, 4, 3, 3))
+        u = np.zeros((N, 12))
+        for k in range(N):
+            for l in range(4):
+                Ri[k, l] = np.eye(3)
+        for j, (k, l) in enumerate(feet):
+            rs = [r for r in range(R) if act[j, r]]
+            if rs:
+                Ga = G[rs]
+                fp, *_ = np.linalg.lstsq(Ga, h[j, rs], rcond=None)
+                _, sv, Vt = np.linalg.svd(Ga)
+                rank = int((sv > 1e-9 * sv[0]).sum())
+                Z = Vt[rank:].T
+            else:
+                fp, Z = np.zeros(3), np.eye(3)
+            Pj = Z @ Z.T
+            Pi[k, l] = Pj
+            Bl[k, l] = Bleg[l] @ Pj
+            Ri[k, l] = np.linalg.inv(Pj @ np.diag(Rh[3 * l:3 * l + 3]) @ Pj + np.eye(3) - Pj)
+            u[k, 3 * l:3 * l + 3] = fp
+        S = factor(Bl, Ri)
+
+        def proj(v):
+            return np.concatenate([np.einsum("kij,kj->ki", Pi[:, l], v[:, 3 * l:3 * l + 3])
+                                   for l in range(4)], axis=1)
+
+        for _ in range(NREF):
+            u = u + lsolve(Bl, Ri, S, -proj(gradient(u)))
+        gr = gradient(u)
+        stat = np.abs(proj(gr)).max()
+        slack = fview(u) @ G.T - h
+        lmin, drop = np.inf, np.zeros_like(act)
+        for j, (k, leg) in enumerate(feet):
+            rs = [r for r in range(R) if act[j, r]]
+            if not rs:
+                continue
+            gf = gr[k, 3 * leg:3 * leg + 3]
+            best, bsub, blam = -np.inf, None, None
+            for sub in itertools.chain.from_iterable(
+                    itertools.combinations(rs, c) for c in range(1, min(3, len(rs)) + 1)):
+                Ga = G[list(sub)]
+                lam_s, *_ = np.linalg.lstsq(Ga.T, gf, rcond=None)
+                if np.abs(Ga.T @ lam_s - gf).max() > 1e-9 * gscale:
+                    continue
+                if lam_s.min() > best:
+                    best, bsub, blam = lam_s.min(), sub, lam_s
+            lmin = min(lmin, best)
+            if bsub is not None and best < -1e-9 * gscale:
+                drop[j, bsub[int(np.argmin(blam))]] = True
+        ok = stat < STAT_TOL * gscale and slack.min() > -1e-9 * hscale and lmin > -1e-9 * gscale
+        info = f"act {int(act.sum())} stat {stat:.2e} slack {slack.min():.2e} lam {lmin:.2e}"
+        return (u if ok else None), info, (act | (slack < -1e-9 * hscale)) & ~drop
+
+    U = np.zeros((N, 12))
+    if nf == 0:
+        return U, 0, 0, True
+    g0 = gradient(np.zeros((N, 12)))
+    gscale = 1.0 + np.abs(g0).max()
+    hscale = 1.0 + np.abs(h).max()
+    # start: minimiser under a mild barrier weight, slacks shifted into the interior
+    Bl, Ri = ipm_blocks(np.full((nf, R), 1e-2))
+    U = lsolve(Bl, Ri, factor(Bl, Ri), -g0)
+    s = np.maximum(fview(U) @ G.T - h, 1.0)
+    lam = np.ones((nf, R))
+    polish_tries = 0
+    for it in range(1, MAX_IT + 1):
+        rd = gradient(U) - gt(lam)
+        rp = fview(U) @ G.T - h - s
+        mu_c = float((s * lam).sum() / m_tot)
+        if verbose:
+            print(f"it {it:2d} rd {np.abs(rd).max():.2e} rp {np.abs(rp).max():.2e} mu {mu_c:.2e}")
+        if mu_c < POLISH_MU * gscale * hscale:
+            polish_tries += 1
+            act = lam > s
+            for corr in range(NCORR + 1):
+                u, info, nact = polish(act)
+                if verbose:
+                    print(f"   polish {polish_tries}.{corr}: {info}")
+                if u is not None:
+                    return u, it, nf, True
+                if np.array_equal(nact, act):
+                    break
+                act = nact
+        D = lam / s
+        Bl, Ri = ipm_blocks(D)
+        S = factor(Bl, Ri)
+
+        def newton(rc):
+            dU = lsolve(Bl, Ri, S, -rd + gt(rc / s - D * rp))
+            ds = fview(dU) @ G.T + rp
+            return dU, ds, (rc - lam * ds) / s
+
+        dU, ds, dl = newton(-s * lam)
+        ap, ad = _max_step(s, ds), _max_step(lam, dl)
+        mu_aff = float(((s + ap * ds) * (lam + ad * dl)).sum() / m_tot)
+        target = max((mu_aff / mu_c) ** 3 * mu_c, MU_FLOOR * gscale * hscale)
+        dU, ds, dl = newton(-s * lam - ds * dl + target)
+        ap = min(1.0, TAU * _max_step(s, ds))
+        ad = min(1.0, TAU * _max_step(lam, dl))
+        U = U + ap * dU
+        s = s + ap * ds
+        lam = lam + ad * dl
+    return U, MAX_IT, nf, False
+
+
+def _max_step(v, dv):
+    neg = dv < 0
+    if not np.any(neg):
+        return 1.0
+    return float(min(1.0, np.min(-v[neg] / dv[neg])))
+
+
+def run_case(bt, b, N, verbose=False):
+    from helpers import oracle_solution, rel_err_u0
+    x, o, _ = oracle_solution(bt, b, N)
+    rec = bt["robot"][b]
+    U, it, nf, ok = solve(o["Ad"], o["Bd"], bt["x0"][b], bt["xref"][b], bt["contact"][b], N,
+                          float(rec[7]), float(rec[8]), rec[9:12], verbose=verbose)
+    return rel_err_u0(U[0], x[:12]), rel_err_u0(U.reshape(-1), x), it, nf, ok
+
+
+def main():
+    worst, iters, fails = 0.0, [], 0
+    cases = []
+    for N in (10, 16, 20):
+        z = np.load(os.path.join(ROOT, "tests", "golden", f"formulation_N{N}.npz"), allow_pickle=False)
+        cases.append((f"golden N={N}", {k: z[k] for k in ("x0", "xref", "contact", "feet", "robot")}, N))
+    from mpcqp.synthetic import make_batch
+    for N in (16, 20):
+        bt = make_batch(8, N, seed=77, gaits=("trot10", "pace10", "bound8"), robots=("a1", "aliengo"),
+                        tilt_deg=15.0)
+        bt["contact"][:4] = 1.0
+        bt["robot"][5, 8] = 40.0
+        bt["robot"][6, 7] = 0.2
+        bt["robot"][7, 7] = 1.5
+        cases.append((f"synth N={N}", bt, N))
+    for name, bt, N in cases:
+        for b in range(len(bt["x0"])):
+            e0, eU, it, nf, ok = run_case(bt, b, N)
+            worst = max(worst, eU)
+            iters.append(it)
+            fails += not ok
+            print(f"{name} b={b:2d} stance={nf:2d} it={it:2d} ok={int(ok)} err u0 {e0:.2e} U {eU:.2e}")
+    print(f"worst {worst:.2e}  iterations mean {np.mean(iters):.1f} max {max(iters)}  unverified {fails}")
+
+
+if __name__ == "__main__":
+    main()
