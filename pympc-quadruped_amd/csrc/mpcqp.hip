@@ -15,6 +15,8 @@
 //                   device queue the first class fills)
 //   class NV = 128: 8 waves, n <= 126                (mpcqp_kernel_128, fed by a
 //                   device queue the first class fills)
+//   large class:    1 wave, n up to 12 N = 240       (mpcqp_kernel_ipm: Riccati-factored
+//                   interior point + exact active-set polish, mpcqp_ipm.h)
 // Formulation in closed form (mpcqp_form.h); H^-1 by a symmetric sweep over
 // register tiles; Goldfarb-Idnani dual active set in projected form with the
 // reduced inverse Hessian and the multiplier map in registers (mpcqp_solve.h).
@@ -28,6 +30,7 @@
 #include <new>
 #include <string>
 #include <utility>
+#include <vector>
 
 #include "mpcqp.h"
 
@@ -276,6 +279,7 @@ __device__ __forceinline__ int wave_argmin_f32(double v, double& vmin_out) {
 
 #include "mpcqp_form.h"
 #include "mpcqp_solve.h"
+#include "mpcqp_ipm.h"
 #include "mpcqp_plan.h"
 
 // Class NV = 64: one 2-wave workgroup per robot of the batch.  Robots with more
@@ -285,11 +289,12 @@ __global__ __launch_bounds__(Cfg<64>::NT) __attribute__((amdgpu_waves_per_eu(2, 
     KParams P, int B, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
-    int* __restrict__ queue, int* __restrict__ queue_big) {
+    int* __restrict__ queue, int* __restrict__ queue_big, int* __restrict__ queue_ipm) {
   __shared__ SharedT<64> sm;
   const int b = blockIdx.x;
   if (b >= B) return;
-  solve_robot<64>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, queue, queue_big);
+  solve_robot<64>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, queue, queue_big,
+                  queue_ipm);
 }
 
 // Class NV = 96: one 6-wave workgroup (4 x 6 register tiles) per robot queued by
@@ -342,17 +347,47 @@ __global__ __launch_bounds__(Cfg<128>::NT) void mpcqp_kernel_128(
   }
 }
 
+// Large class (n > 128: standing schedules at N >= 11): one wave per queued robot,
+// Riccati-factored interior point + active-set polish (mpcqp_ipm.h).  Same launch /
+// reset protocol as class 128.
+__global__ __launch_bounds__(LANES) void mpcqp_kernel_ipm(
+    KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
+    const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
+    float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
+    int* __restrict__ queue) {
+  __shared__ IpmShared sm;
+  const int tid = threadIdx.x;
+  const int k = blockIdx.x;
+  const int cnt = uni(__hip_atomic_load(&queue[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (k < cnt) {
+    const int b = uni(queue[4 + k]);
+    solve_robot_ipm(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg);
+    if (tid == 0 && atomicAdd(&queue[2], 1) == cnt - 1) {
+      atomicExch(&queue[0], 0);
+      atomicExch(&queue[2], 0);
+    }
+  }
+}
+
 }  // namespace
 
 // ============================================================== C ABI
+// Device queues of one stream: three queues of [count, next, finished, pad, robots...
+// (cap)] -- class 64 -> class 96, -> class 128, -> the interior-point class.  Calls on
+// one stream are ordered, so the count / reset protocol of the queued kernels is
+// safe; calls on different streams of one context use different queue sets.
+struct QueueSet {
+  hipStream_t stream;
+  int cap;
+  int* buf;
+};
+
 struct mpcqp_ctx {
   mpcqp_params params;
   int device;
   int stance_hint;
   int ncu;
-  int qcap;           // robots the device queue can hold
-  int* queue;         // two queues of [count, next, finished, pad, robots... (qcap)]:
-                      // class 64 -> class 96, class 96 -> class 128
+  std::vector<QueueSet> queues;
   double dt_control;  // planner constants (mpcqp_set_planner)
   double gravity;
   double max_pos_error;
@@ -362,6 +397,58 @@ struct mpcqp_ctx {
 static int set_err(mpcqp_ctx* ctx, int code, const std::string& msg) {
   if (ctx) ctx->err = msg;
   return code;
+}
+
+// Makes the context's device current for one ABI call and restores the caller's.
+struct DeviceScope {
+  int prev = -1;
+  bool ok = false;
+  explicit DeviceScope(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceScope() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// The queue set of `st`, holding at least `batch` robots per queue (grown on demand;
+// the old buffer is freed once the stream's earlier launches are done).
+static int* stream_queues(mpcqp_ctx* ctx, hipStream_t st, int batch, int* err, int* cap) {
+  *err = MPCQP_OK;
+  QueueSet* qs = nullptr;
+  for (auto& q : ctx->queues)
+    if (q.stream == st) qs = &q;
+  if (qs && qs->cap >= batch) {
+    *cap = qs->cap;
+    return qs->buf;
+  }
+  if (!qs) {
+    ctx->queues.push_back(QueueSet{st, 0, nullptr});
+    qs = &ctx->queues.back();
+  }
+  if (qs->buf) {
+    if (hipStreamSynchronize(st) != hipSuccess) {
+      *err = set_err(ctx, MPCQP_ERR_HIP, "queue growth: stream sync failed");
+      return nullptr;
+    }
+    (void)hipFree(qs->buf);
+    qs->buf = nullptr;
+    qs->cap = 0;
+  }
+  const size_t bytes = sizeof(int) * 3 * (4 + (size_t)batch);
+  if (hipMalloc(&qs->buf, bytes) != hipSuccess) {
+    qs->buf = nullptr;
+    *err = set_err(ctx, MPCQP_ERR_ALLOC, "queue allocation failed");
+    return nullptr;
+  }
+  if (hipMemsetAsync(qs->buf, 0, bytes, st) != hipSuccess) {
+    *err = set_err(ctx, MPCQP_ERR_HIP, "queue init failed");
+    return nullptr;
+  }
+  qs->cap = batch;
+  *cap = batch;
+  return qs->buf;
 }
 
 extern "C" {
@@ -391,8 +478,6 @@ int mpcqp_create(const mpcqp_params* p, int32_t device, mpcqp_ctx** out) {
   ctx->params = *p;
   ctx->device = device;
   ctx->stance_hint = 0;
-  ctx->queue = nullptr;
-  ctx->qcap = 0;
   ctx->ncu = 0;
   ctx->dt_control = 0.001;    // linear_mpc_configs.py:6
   ctx->gravity = 9.81;        // linear_mpc_configs.py:13
@@ -418,7 +503,8 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   if (batch == 0) return MPCQP_OK;
   if (!x0 || !xref || !contact || !feet || !robot || !u0)
     return set_err(ctx, MPCQP_ERR_ARG, "null input/output pointer");
-  if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, "hipSetDevice failed");
+  DeviceScope dev(ctx->device);
+  if (!dev.ok) return set_err(ctx, MPCQP_ERR_HIP, "hipSetDevice failed");
   KParams kp;
   kp.N = ctx->params.horizon;
   kp.max_iter = ctx->params.max_iter;
@@ -426,30 +512,31 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   for (int i = 0; i < NX; ++i) kp.q[i] = ctx->params.q_diag[i];
   for (int i = 0; i < NU; ++i) kp.r[i] = ctx->params.r_diag[i];
   hipStream_t st = (hipStream_t)stream;
-  // robots with more than 64 stance variables are queued for class 96, those with
-  // more than 96 on for class 128 -- unless the caller promised (stance hint) that
-  // none exceeds the smaller class
-  const bool large = !(ctx->stance_hint > 0 && 3 * ctx->stance_hint <= 64);
-  const bool huge = large && !(ctx->stance_hint > 0 && 3 * ctx->stance_hint <= 96);
-  if (large && batch > ctx->qcap) {
-    if (ctx->queue) (void)hipFree(ctx->queue);
-    ctx->queue = nullptr;
-    ctx->qcap = 0;
-    if (hipMalloc(&ctx->queue, sizeof(int) * 2 * (4 + (size_t)batch)) != hipSuccess)
-      return set_err(ctx, MPCQP_ERR_ALLOC, "queue allocation failed");
-    if (hipMemset(ctx->queue, 0, sizeof(int) * 2 * (4 + (size_t)batch)) != hipSuccess)
-      return set_err(ctx, MPCQP_ERR_HIP, "queue init failed");
-    ctx->qcap = batch;
+  // A robot has n = 3 * #stance <= 12 N variables.  Robots with more than 64 are queued
+  // for class 96, more than 96 for class 128, more than 128 for the interior-point
+  // class -- each queued launch skipped when no robot can need it (horizon, or the
+  // caller's stance hint).
+  const int nmax_h = 12 * kp.N;
+  const int nmax = ctx->stance_hint > 0 && 3 * ctx->stance_hint < nmax_h ? 3 * ctx->stance_hint : nmax_h;
+  const bool large = nmax > 64, huge = nmax > 96, giant = nmax > 128;
+  int* q = nullptr;
+  int cap = 0;
+  if (large) {
+    int qerr = MPCQP_OK;
+    q = stream_queues(ctx, st, batch, &qerr, &cap);
+    if (!q) return qerr;
   }
-  int* q = large ? ctx->queue : nullptr;
-  int* q2 = huge ? ctx->queue + 4 + ctx->qcap : nullptr;
+  const size_t qstride = 4 + (size_t)cap;   // the set's layout: three queues of 4 + cap ints
+  int* q1 = large ? q : nullptr;
+  int* q2 = huge ? q + qstride : nullptr;
+  int* q3 = giant ? q + 2 * qstride : nullptr;
   hipLaunchKernelGGL(mpcqp_kernel_64, dim3(batch), dim3(Cfg<64>::NT), 0, st, kp, (int)batch, x0, xref, contact,
-                     feet, robot, u0, U, (int*)status, (int*)iters, q, q2);
+                     feet, robot, u0, U, (int*)status, (int*)iters, q1, q2, q3);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch: ") + hipGetErrorString(e));
   if (large) {
     hipLaunchKernelGGL(mpcqp_kernel_96, dim3(batch), dim3(Cfg<96>::NT), 0, st, kp, x0, xref, contact, feet, robot,
-                       u0, U, (int*)status, (int*)iters, q, q2);
+                       u0, U, (int*)status, (int*)iters, q1, q2);
     e = hipGetLastError();
     if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (96): ") + hipGetErrorString(e));
   }
@@ -458,6 +545,12 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
                        u0, U, (int*)status, (int*)iters, q2);
     e = hipGetLastError();
     if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (128): ") + hipGetErrorString(e));
+  }
+  if (giant) {
+    hipLaunchKernelGGL(mpcqp_kernel_ipm, dim3(batch), dim3(LANES), 0, st, kp, x0, xref, contact, feet, robot, u0, U,
+                       (int*)status, (int*)iters, q3);
+    e = hipGetLastError();
+    if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (ipm): ") + hipGetErrorString(e));
   }
   return MPCQP_OK;
 }
@@ -488,7 +581,8 @@ static int launch_plan(mpcqp_ctx* ctx, int32_t batch, int32_t flags, int root_la
     return set_err(ctx, MPCQP_ERR_ARG, "null height/xref pointer on an MPC tick");
   if (mpc_tick && gait && (!iteration || !contact))
     return set_err(ctx, MPCQP_ERR_ARG, "gait given without iteration/contact");
-  if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, "hipSetDevice failed");
+  DeviceScope dev(ctx->device);
+  if (!dev.ok) return set_err(ctx, MPCQP_ERR_HIP, "hipSetDevice failed");
   PlanParams pp;
   pp.N = ctx->params.horizon;
   pp.mpc_tick = mpc_tick;
@@ -529,7 +623,8 @@ int mpcqp_stance_torques(mpcqp_ctx* ctx, int32_t batch, const float* jac, const 
   if (batch < 0 || contact_stride < 4) return set_err(ctx, MPCQP_ERR_ARG, "batch < 0 or contact_stride < 4");
   if (batch == 0) return MPCQP_OK;
   if (!jac || !contact || !u0 || !tau) return set_err(ctx, MPCQP_ERR_ARG, "null torque pointer");
-  if (hipSetDevice(ctx->device) != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, "hipSetDevice failed");
+  DeviceScope dev(ctx->device);
+  if (!dev.ok) return set_err(ctx, MPCQP_ERR_HIP, "hipSetDevice failed");
   const int threads = (int)batch * 12;
   hipLaunchKernelGGL(mpcqp_stance_torque_kernel, dim3((threads + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                      (int)batch, jac, contact, (int)contact_stride, u0, tau);
@@ -539,7 +634,14 @@ int mpcqp_stance_torques(mpcqp_ctx* ctx, int32_t batch, const float* jac, const 
 }
 
 int mpcqp_destroy(mpcqp_ctx* ctx) {
-  if (ctx && ctx->queue) (void)hipFree(ctx->queue);
+  if (ctx) {
+    DeviceScope dev(ctx->device);
+    for (auto& q : ctx->queues)
+      if (q.buf) {
+        (void)hipStreamSynchronize(q.stream);
+        (void)hipFree(q.buf);
+      }
+  }
   delete ctx;
   return MPCQP_OK;
 }

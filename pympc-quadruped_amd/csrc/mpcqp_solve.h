@@ -169,15 +169,16 @@ __device__ __forceinline__ void write_empty_t(int b, int tid, int N, int code, f
 }
 
 // One robot.  A robot exceeding NV is appended to `queue` (when given) for the
-// next capacity class -- or to `queue_big` for the one after, when it exceeds
-// that too -- otherwise reported MPCQP_STATUS_TOO_LARGE.
+// next capacity class -- or to `queue_big` / `queue_ipm` for the ones after, when
+// it exceeds those too -- otherwise reported MPCQP_STATUS_TOO_LARGE.
 template <int NV>
 __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>& sm, const float* __restrict__ x0g,
                                             const float* __restrict__ xrefg, const float* __restrict__ contactg,
                                             const float* __restrict__ feetg, const float* __restrict__ robotg,
                                             float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg,
                                             int* __restrict__ itersg, int* __restrict__ queue,
-                                            int* __restrict__ queue_big = nullptr) {
+                                            int* __restrict__ queue_big = nullptr,
+                                            int* __restrict__ queue_ipm = nullptr) {
   using C = Cfg<NV>;
   constexpr int NT = C::NT, TCN = C::TCN, CPL = C::CPL, VPL = C::VPL, RPW = C::RPW, TW = C::TW;
   const int tid = threadIdx.x;
@@ -203,9 +204,11 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   const int S = uni(sm.mt.S);
   const int n = 3 * S, m = 6 * S;
   if (n > NV) {
-    // the next capacity class takes it: `queue`, or `queue_big` (when given) for a
-    // robot beyond class 96 as well
-    int* const qn = (queue_big && n > 96) ? queue_big : queue;
+    // the next capacity class takes it: `queue`, `queue_big` (when given) for a robot
+    // beyond class 96 as well, `queue_ipm` (when given) for one beyond class 128
+    int* qn = queue;
+    if (queue_big && n > 96) qn = queue_big;
+    if (queue_ipm && n > 128) qn = queue_ipm;
     if (qn) {
       if (tid == 0) qn[4 + atomicAdd(&qn[0], 1)] = b;
       return;

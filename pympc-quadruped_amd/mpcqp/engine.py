@@ -115,6 +115,17 @@ class LinearMpc:
         st = torch.as_tensor(state)
         B = int(st.shape[0]) if st.dim() == 2 else 1
         N = self.horizon
+        cur = torch.cuda.current_stream(self.device)
+        if stream is None:
+            stream = cur
+        elif stream != cur:
+            # inputs produced (or copied below) on the current stream must be ready
+            # before the launch stream reads them
+            stream.wait_stream(cur)
+        with torch.cuda.stream(stream):
+            return self._solve_on(stream, state, xref, contact_schedule, feet, robot, return_all, B, N)
+
+    def _solve_on(self, stream, state, xref, contact_schedule, feet, robot, return_all, B, N):
         x0 = self._dev(state, (B, 13), "state")
         xr = self._dev(xref, (B, N, 13), "xref")
         ct = self._dev(contact_schedule, (B, N, 4), "contact_schedule")
@@ -135,12 +146,15 @@ class LinearMpc:
         U = torch.empty((B, N, 12), dtype=torch.float32, device=self.device) if return_all else None
         status = torch.empty((B,), dtype=torch.int32, device=self.device)
         iters = torch.empty((B,), dtype=torch.int32, device=self.device)
-        if stream is None:
-            stream = torch.cuda.current_stream(self.device)
         code = self.lib.mpcqp_solve(self._ctx, B, _ptr(x0), _ptr(xr), _ptr(ct), _ptr(ft), _ptr(rb),
                                     _ptr(u0), _ptr(U), _ptr(status), _ptr(iters),
                                     ctypes.c_void_p(stream.cuda_stream))
         _lib.check(self._ctx, code, "mpcqp_solve")
+        # the caching allocator must not hand these blocks to other streams' work
+        # before the launch has finished with them
+        for t in (x0, xr, ct, ft, rb, u0, U, status, iters):
+            if t is not None and t.numel():
+                t.record_stream(stream)
         if return_all:
             return SolveResult(u0, U, status, iters)
         return u0

@@ -10,7 +10,6 @@ from helpers import oracle_solution, rel_err_u0
 
 TOL_U0 = 1e-4   # north_star: GRF within 1e-4 relative, norm-wise ||du0||_inf / ||u0*||_inf
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
-NV_MAX = 126    # stance variables this build solves (n = 3 * #stance; 64 per wave kernel, 126 per 8-wave class)
 
 pytestmark = pytest.mark.gpu
 
@@ -49,21 +48,15 @@ def test_u0_matches_oracle(N, gaits, robots, tilt):
 
 @pytest.mark.parametrize("N", [10, 16, 20])
 def test_reference_golden_fixtures(N):
-    """u* of QPs built by the reference's own functions (tests/golden/make_golden.py)."""
+    """u* of QPs built by the reference's own functions (tests/golden/make_golden.py):
+    every case, standing schedules (n = 192 / 240, the interior-point class) included."""
     z = np.load(os.path.join(GOLDEN, f"formulation_N{N}.npz"), allow_pickle=False)
     bt = {k: z[k] for k in ("x0", "xref", "contact", "feet", "robot")}
     u0, U, status, _ = _solve(_engine(N), bt)
-    n_eff = 3 * (bt["contact"] > 0).reshape(len(bt["x0"]), -1).sum(1)
-    checked = 0
     for b in range(len(bt["x0"])):
-        if n_eff[b] > NV_MAX:
-            assert status[b] == 3   # MPCQP_STATUS_TOO_LARGE: reported, never silently wrong
-            continue
-        assert status[b] == 0
+        assert status[b] == 0, (b, status)
         assert rel_err_u0(u0[b], z["u_star"][b][:12]) < TOL_U0, (b, u0[b], z["u_star"][b][:12])
-        assert rel_err_u0(U[b], z["u_star"][b]) < TOL_U0
-        checked += 1
-    assert checked >= 4
+        assert rel_err_u0(U[b], z["u_star"][b]) < TOL_U0, b
 
 
 def test_edge_cases():
@@ -87,12 +80,14 @@ def test_edge_cases():
     for b in (4, 5):
         x, _, _ = oracle_solution(bt, b, N)
         assert status[b] == 0 and rel_err_u0(u0[b], x[:12]) < TOL_U0
-    # beyond capacity: standing at N = 20 (n = 240 > 126) is reported, never wrong
+    # standing at N = 20 (n = 240): the interior-point class, next to two class-128 robots
     bt20 = make_batch(3, 20, seed=6, gaits=("trot10",), robots=("a1",))
     bt20["contact"][1] = 1.0
-    u20, _, st20, _ = _solve(_engine(20), bt20)
-    assert st20[1] == 3 and np.all(u20[1] == 0)
-    assert st20[0] == 0 and st20[2] == 0
+    u20, U20, st20, _ = _solve(_engine(20), bt20)
+    assert (st20 == 0).all(), st20
+    for b in range(3):
+        x, _, _ = oracle_solution(bt20, b, 20)
+        assert rel_err_u0(u20[b], x[:12]) < TOL_U0 and rel_err_u0(U20[b], x) < TOL_U0, b
     eng = _engine(N)
     empty = {k: v[:0] for k, v in bt.items()}
     out = eng.solve(empty["x0"], empty["xref"], empty["contact"], empty["feet"], robot=empty["robot"])
@@ -101,13 +96,12 @@ def test_edge_cases():
 
 @pytest.mark.parametrize("N", [10, 16])
 def test_deterministic_and_stream_ordered(N):
-    """Repeated launches (the large-class queue resets itself) and other streams
+    """Repeated launches (the queued classes reset their queues) and other streams
     give bitwise-identical results."""
     import torch
     from mpcqp.synthetic import make_batch
     bt = make_batch(256, N, seed=9, gaits=("trot10", "pace10", "bound8"), robots=("a1",))
-    if N == 10:
-        bt["contact"][::7] = 1.0   # some standing robots: both kernels in one call
+    bt["contact"][::7] = 1.0   # some standing robots: every queued class in one call
     eng = _engine(N)
     a = _solve(eng, bt)
     a2 = _solve(eng, bt)
@@ -121,9 +115,10 @@ def test_deterministic_and_stream_ordered(N):
 
 def test_full_size_properties():
     """Every bench config's per-GPU shape (2: 1024 x N10, 3: 4096 x N10 mixed, 4: 2048 x
-    N16, 5: 8192 x N20 mixed A1/Aliengo with tilted cones): size-independent properties of every
-    solution -- feasibility of every cone row, swing GRFs exactly 0, status OK --
-    plus oracle parity on a sample."""
+    N16, 5: 8192 x N20 mixed A1/Aliengo with tilted cones; configs 4 and 5 with every
+    16th robot standing -- the interior-point class): size-independent properties of
+    every solution -- feasibility of every cone row, swing GRFs exactly 0, status OK --
+    plus oracle parity on a sample that includes standing robots."""
     from mpcqp.synthetic import make_batch
     mu = 0.7
     for B, N, gaits, robots, tilt in ((1024, 10, ("trot10",), ("a1",), 0.0),
@@ -131,6 +126,8 @@ def test_full_size_properties():
                                       (2048, 16, ("trot10", "pace10", "bound8"), ("a1",), 0.0),
                                       (8192, 20, ("trot10", "pace10", "bound8"), ("a1", "aliengo"), 15.0)):
         bt = make_batch(B, N, seed=2024, gaits=gaits, robots=robots, tilt_deg=tilt)
+        if N > 10:
+            bt["contact"][::16] = 1.0   # standing (mpc scripts start in Gait.STANDING)
         u0, U, status, iters = _solve(_engine(N), bt)
         assert (status == 0).all(), (N, np.unique(status, return_counts=True))
         f = U.reshape(B, N, 4, 3)
@@ -148,7 +145,7 @@ def test_full_size_properties():
         tol = 1e-4 * (1.0 + np.abs(f).max(axis=(1, 2, 3)))[:, None, None]
         assert np.all(fn >= -tol) and np.all(fn <= 500.0 + tol)
         assert np.all(np.abs(f1) <= mu * fn + tol) and np.all(np.abs(f2) <= mu * fn + tol)
-        for b in range(0, B, B // 8):
+        for b in list(range(0, B, B // 8)) + [B // 2 + 1, B - 3]:
             x, _, _ = oracle_solution(bt, b, N)
             assert rel_err_u0(u0[b], x[:12]) < TOL_U0, (N, b)
 
@@ -179,7 +176,7 @@ def test_binding_bounds_and_friction_extremes(N):
 
 def test_capacity_class_routing():
     """One N = 16 call reaching every capacity class: n = 96 (class 96), n = 114 and
-    126 (class 128), n = 60 (class 64) and standing n = 192 (MPCQP_STATUS_TOO_LARGE),
+    126 (class 128), n = 60 (class 64) and standing n = 192 (the interior-point class),
     then twice more (the device queues reset themselves), and with a stance hint the
     batch breaks (the promise is the caller's: the robot beyond it is reported)."""
     from mpcqp.synthetic import make_batch
@@ -194,8 +191,7 @@ def test_capacity_class_routing():
     eng = _engine(N)
     for _ in range(3):
         u0, U, status, _ = _solve(eng, bt)
-        assert status[4] == 3 and np.all(u0[4] == 0)
-        for b in (0, 1, 2, 3, 5):
+        for b in (0, 1, 2, 3, 4, 5):
             assert status[b] == 0, (b, status)
             x, _, _ = oracle_solution(bt, b, N)
             assert rel_err_u0(U[b], x) < TOL_U0, b
@@ -203,3 +199,35 @@ def test_capacity_class_routing():
     _, _, st, _ = _solve(hinted, bt)
     assert st[1] == 3 and st[2] == 3 and st[4] == 3
     assert all(st[b] == 0 for b in (0, 3, 5, 6, 7))
+
+
+def test_two_streams_no_host_sync():
+    """One context, two streams, no host synchronisation between the calls: each
+    stream has its own device queues, so robots of the queued classes (N = 16 trot /
+    pace / bound -> class 96, standing -> the interior-point class) never mix."""
+    import torch
+    from mpcqp.synthetic import make_batch
+    N = 16
+    eng = _engine(N)
+    bts = []
+    for seed in (51, 52):
+        bt = make_batch(96, N, seed=seed, gaits=("trot10", "pace10", "bound8"), robots=("a1",))
+        bt["contact"][seed % 5::9] = 1.0
+        bts.append(bt)
+    dev = torch.device("cuda:0")
+    ins = [{k: torch.as_tensor(v).to(dev) for k, v in bt.items()} for bt in bts]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    for s, t in zip(streams, ins):
+        with torch.cuda.stream(s):
+            outs.append(eng.solve(t["x0"], t["xref"], t["contact"], t["feet"], robot=t["robot"],
+                                  return_all=True, stream=s))
+    torch.cuda.synchronize()
+    for bt, res in zip(bts, outs):
+        status = res.status.cpu().numpy()
+        U = res.U.cpu().numpy().reshape(len(bt["x0"]), -1)
+        assert (status == 0).all(), status
+        for b in range(0, len(bt["x0"]), 7):
+            x, _, _ = oracle_solution(bt, b, N)
+            assert rel_err_u0(U[b], x) < TOL_U0, b

@@ -1,0 +1,59 @@
+"""GPU diagnostic for the interior-point class: runs golden standing cases through a
+-DMPCQP_IPM_DEBUG build (tools/libmpcqp_ipmdbg.so, built by `python tools/ipm_debug.py
+build` on the CPU) and prints the per-iteration trace next to the release build's error."""
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "pympc-quadruped_amd"), os.path.join(ROOT, "tests")]
+DBG = os.path.join(ROOT, "tools", "libmpcqp_ipmdbg.so")
+
+if len(sys.argv) > 1 and sys.argv[1] == "build":
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                    "-DMPCQP_IPM_DEBUG", "-I" + os.path.join(ROOT, "include"), "-o", DBG,
+                    os.path.join(ROOT, "pympc-quadruped_amd", "csrc", "mpcqp.hip")], check=True)
+    sys.exit(0)
+
+import torch  # noqa: E402
+from mpcqp import _lib  # noqa: E402
+from helpers import rel_err_u0  # noqa: E402
+
+N = int(os.environ.get("N", "16"))
+cases = [int(c) for c in os.environ.get("CASES", "5,6,15").split(",")]
+z = np.load(os.path.join(ROOT, "tests", "golden", f"formulation_N{N}.npz"), allow_pickle=False)
+bt = {k: z[k][cases] for k in ("x0", "xref", "contact", "feet", "robot")}
+# debug build: same call through the diagnostic library
+lib = ctypes.CDLL(DBG)
+params = _lib.MpcqpParams()
+lib.mpcqp_default_params.argtypes = [ctypes.c_void_p, ctypes.c_int]
+lib.mpcqp_default_params(ctypes.byref(params), N)
+ctx = ctypes.c_void_p()
+lib.mpcqp_create.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+assert lib.mpcqp_create(ctypes.byref(params), 0, ctypes.byref(ctx)) == 0
+dev = torch.device("cuda:0")
+t = {k: torch.as_tensor(np.ascontiguousarray(v, dtype=np.float32)).to(dev) for k, v in bt.items()}
+B = len(cases)
+u0d = torch.empty((B, 12), device=dev)
+Ud = torch.zeros((B, N * 12), device=dev)
+st = torch.empty((B,), dtype=torch.int32, device=dev)
+itd = torch.empty((B,), dtype=torch.int32, device=dev)
+p = lambda x: ctypes.c_void_p(x.data_ptr())
+lib.mpcqp_solve.argtypes = [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 10
+rc = lib.mpcqp_solve(ctx, B, p(t["x0"]), p(t["xref"]), p(t["contact"]), p(t["feet"]), p(t["robot"]), p(u0d),
+                     p(Ud), p(st), p(itd), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+torch.cuda.synchronize()
+assert rc == 0, rc
+D = Ud.cpu().numpy()
+for i, c in enumerate(cases):
+    print(f"--- case {c} trace (it, mu, rd, rp, stat/g, slack min, lam min, code am*1000+nq*100+ndet, min res)")
+    tr = D[i][:N * 12 // 9 * 9].reshape(-1, 9)
+    for row in tr:
+        if row[0] == 0:
+            break
+        print("  " + " ".join(f"{v:10.3e}" for v in row))
+lib.mpcqp_destroy.argtypes = [ctypes.c_void_p]
+lib.mpcqp_destroy(ctx)
