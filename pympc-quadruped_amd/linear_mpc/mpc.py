@@ -19,8 +19,11 @@ Behaviour kept from the reference:
   * the solver string is asserted (mpc.py:264); 'drake' and 'qpsolvers' both
     solve the two-sided Drake-branch QP (the reference's qpsolvers branch drops
     lb, SURVEY D3), 'hip' is accepted as well;
-  * an unsuccessful solve still returns the best iterate (mpc.py:284-286 never
-    checks is_success); a warning is emitted instead of silence.
+  * an unsuccessful solve (iteration cap) still returns the best iterate
+    (mpc.py:284-286 never checks is_success), with a warning; non-finite inputs
+    raise (there is no iterate to return);
+  * Q and R must be diagonal (the reference's are, linear_mpc_configs.py:19-20);
+    a weight with off-diagonal entries raises instead of being truncated.
 """
 import math
 import os
@@ -45,6 +48,22 @@ def quat2ZYXangle(quat):
     return [roll, pitch, yaw]
 
 
+def _diagonal_weights(W, n, name):
+    """The diagonal of LinearMpcConfig.Q / .R (mpc.py:50,52 build Qbar = kron(I_N, Q)).
+    The engine's closed-form condensing needs a diagonal weight: a matrix with
+    off-diagonal entries is rejected rather than silently truncated."""
+    W = np.asarray(W, dtype=np.float64)
+    if W.ndim == 1 and W.shape == (n,):
+        return W.copy()
+    if W.shape != (n, n):
+        raise ValueError(f"{name} must be {n}x{n} (or its diagonal), got {W.shape}")
+    off = W - np.diag(np.diag(W))
+    if np.any(off != 0.0):
+        raise ValueError(f"{name} has off-diagonal entries; the engine supports diagonal weights "
+                         f"only (the reference configs are diagonal, linear_mpc_configs.py:19-20)")
+    return np.diag(W).copy()
+
+
 class ModelPredictiveController():
 
     def __init__(self, mpc_config, robot_config):
@@ -67,8 +86,8 @@ class ModelPredictiveController():
         self.base_inertia_base = robot_config.base_inertia_base
         self.mass = robot_config.mass_base
         self.com_height_des = robot_config.base_height_des
-        self.q_diag = np.diag(np.asarray(mpc_config.Q, dtype=np.float64)).copy()
-        self.r_diag = np.diag(np.asarray(mpc_config.R, dtype=np.float64)).copy()
+        self.q_diag = _diagonal_weights(mpc_config.Q, 13, "Q")
+        self.r_diag = _diagonal_weights(mpc_config.R, 12, "R")
         I = np.asarray(self.base_inertia_base, dtype=np.float32)
         self._robot_record = pack_robot(
             dict(mass=float(self.mass), fz_max=float(self.fz_max), mu=float(self.mu),
@@ -87,6 +106,7 @@ class ModelPredictiveController():
             self._dev = dict(
                 plan_state=torch.zeros((1, PLAN_STRIDE), dtype=torch.float64, device=d),
                 x0=torch.zeros((1, 13), **f32), xref=torch.zeros((1, self.horizon, 13), **f32),
+                xref_gen=torch.zeros((1, self.horizon, 13), **f32),
                 height=torch.full((1,), float(self.com_height_des), **f32),
                 robot=torch.as_tensor(self._robot_record).reshape(1, -1).to(d))
             self._engine = e
@@ -105,13 +125,13 @@ class ModelPredictiveController():
         t = torch.from_numpy(host).to(d)
         return dict(quat=t[0:4], pos=t[4:7], omega=t[7:10], vel=t[10:13], rot=t[13:22])
 
-    def _plan(self, flags, vel_base_des_body, yaw_turn_rate):
+    def _plan(self, flags, vel_base_des_body, yaw_turn_rate, xref_key="xref"):
         import torch
         e = self._get_engine()
         dv = self._dev
         vb = torch.as_tensor(np.asarray(vel_base_des_body, dtype=np.float64).reshape(1, 3)).to(e.device)
         yr = torch.full((1,), float(yaw_turn_rate), dtype=torch.float64, device=e.device)
-        e.plan(flags, dv["plan_state"], dv["x0"], vb, yr, height_des=dv["height"], xref=dv["xref"],
+        e.plan(flags, dv["plan_state"], dv["x0"], vb, yr, height_des=dv["height"], xref=dv[xref_key],
                **self._planner_inputs())
 
     def _planner_state(self):
@@ -159,13 +179,20 @@ class ModelPredictiveController():
             self._plan(PLAN_REFERENCE, self._base_vel_base_des, yaw_turn_rate_des)
             self.is_first_run = False
             self.__contact_forces = self._solve_mpc(self._dev["xref"], gait_table, solver=solver)[0:12]
-            self.ref_traj = self._dev["xref"].cpu().numpy().reshape(-1)
+            self._ref_traj_host = None   # ref_traj (mpc.py:97) is read back only when asked for
             if debug and iter_counter == iter_debug:
                 warnings.warn("debug CoM-trajectory plot (mpc.py:293-318) is not provided by the engine")
         else:
             self._plan(0, self._base_vel_base_des, yaw_turn_rate_des)
             self.is_first_run = False
         return self.__contact_forces[0:12]
+
+    @property
+    def ref_traj(self):
+        """X_ref of the last MPC tick (mpc.py:96-97), float32 [13N]."""
+        if getattr(self, "_ref_traj_host", None) is None:
+            self._ref_traj_host = self._dev["xref"].cpu().numpy().reshape(-1)
+        return self._ref_traj_host
 
     def generate_reference_trajectory(self, vel_base_des, yaw_turn_rate):
         """mpc.py:110-170 alone (stateful clamp + roll/pitch compensation), on the device.
@@ -175,8 +202,9 @@ class ModelPredictiveController():
         from mpcqp._lib import PLAN_NO_INTEGRATE, PLAN_REFERENCE
         R = np.asarray(self.__robot_data.R_base, dtype=np.float64).reshape(3, 3)
         vb = np.linalg.solve(R, np.asarray(vel_base_des, dtype=np.float64).reshape(3))
-        self._plan(PLAN_REFERENCE | PLAN_NO_INTEGRATE, vb, yaw_turn_rate)
-        return self._dev["xref"].cpu().numpy().reshape(-1)
+        # its own X_ref buffer: ref_traj keeps the last MPC tick's (mpc.py:96-97)
+        self._plan(PLAN_REFERENCE | PLAN_NO_INTEGRATE, vb, yaw_turn_rate, xref_key="xref_gen")
+        return self._dev["xref_gen"].cpu().numpy().reshape(-1)
 
     def _solve_mpc(self, ref_traj, gait_table, solver='drake', debug=False):
         """mpc.py:262-290 -> one engine call; returns U[12N] (float64, like Drake).
@@ -184,15 +212,28 @@ class ModelPredictiveController():
         x0 is the device state the planner packed this iteration; ``ref_traj`` may be
         the planner's device X_ref or a host array."""
         assert solver == 'drake' or solver == 'qpsolvers' or solver == 'hip'
+        import torch
         e = self._get_engine()
+        table = np.asarray(gait_table, dtype=np.float32).reshape(-1)
         feet = np.asarray([np.asarray(f, dtype=np.float64).reshape(3) for f in self.pos_base_feet],
-                          dtype=np.float32)
+                          dtype=np.float32).reshape(-1)
+        # one host->device copy for the gait table and the foot positions
+        hostin = torch.from_numpy(np.concatenate([table, feet]))
+        devin = hostin.to(e.device, non_blocking=False)
+        # the exact stance count of this table: the engine launches only the capacity
+        # classes it can need
+        e.set_stance_hint(int(np.count_nonzero(table > 0)))
         res = e.solve(self._dev["x0"], ref_traj if not isinstance(ref_traj, np.ndarray)
                       else np.asarray(ref_traj, dtype=np.float32)[None, :],
-                      np.asarray(gait_table, dtype=np.float32)[None, :], feet[None, :, :],
+                      devin[:table.size].reshape(1, -1), devin[table.size:].reshape(1, 4, 3),
                       robot=self._dev["robot"], return_all=True)
-        U = res.U.cpu().numpy().reshape(-1).astype(np.float64)
-        status = int(res.status.cpu().numpy()[0])
+        # one device->host copy (and one synchronisation) for U and the status
+        out = torch.cat([res.U.reshape(-1), res.status.to(torch.float32)]).cpu().numpy()
+        U = out[:-1].astype(np.float64)
+        status = int(out[-1])
+        if status == 3 or status == 4:   # MPCQP_STATUS_TOO_LARGE / NONFINITE: no usable forces
+            raise RuntimeError(f"mpcqp: robot solve failed with status {status}")
         if status != 0:
+            # mpc.py:284-286 never checks is_success; the best iterate is returned, loudly
             warnings.warn(f"mpcqp: robot solve status {status}; returning the best iterate")
         return U

@@ -19,6 +19,19 @@ from . import _lib
 from .params import (DT_MPC, Q_DIAG, R_DIAG, ROBOT_PRESETS, ROBOT_STRIDE, pack_robot)
 
 
+def _diag(W, n, name):
+    """Diagonal weights from a length-n vector or an n x n diagonal matrix; off-diagonal
+    entries raise (the closed-form condensing assumes diagonal Q / R, mpc.py:50,52)."""
+    W = np.asarray(W, dtype=np.float64)
+    if W.shape == (n,):
+        return W
+    if W.shape == (n, n):
+        if np.any(W - np.diag(np.diag(W)) != 0.0):
+            raise ValueError(f"{name} has off-diagonal entries: only diagonal weights are supported")
+        return np.diag(W)
+    raise ValueError(f"{name}: expected ({n},) or ({n}, {n}), got {W.shape}")
+
+
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
@@ -55,9 +68,9 @@ class LinearMpc:
         p = _lib.default_params(self.horizon)
         p.dt = float(dt)
         p.max_iter = int(max_iter)
-        for i, v in enumerate(np.asarray(Q, dtype=np.float64).reshape(-1)):
+        for i, v in enumerate(_diag(Q, 13, "Q")):
             p.q_diag[i] = float(v)
-        for i, v in enumerate(np.asarray(R, dtype=np.float64).reshape(-1)):
+        for i, v in enumerate(_diag(R, 12, "R")):
             p.r_diag[i] = float(v)
         self.params = p
         ctx = ctypes.c_void_p()
@@ -65,9 +78,18 @@ class LinearMpc:
         _lib.check(None, self.lib.mpcqp_create(ctypes.byref(p), int(idx), ctypes.byref(ctx)),
                    "mpcqp_create")
         self._ctx = ctx
+        self._hint = 0
         if max_stance:
-            _lib.check(ctx, self.lib.mpcqp_set_stance_hint(ctx, int(max_stance)), "set_stance_hint")
+            self.set_stance_hint(max_stance)
         self.default_robot = self._robot_record(robot)
+
+    def set_stance_hint(self, max_stance):
+        """Promise at most ``max_stance`` stance foot-steps per robot in the following
+        solves (0 = no promise): capacity classes above 3 * max_stance variables are
+        not launched.  A robot breaking the promise gets MPCQP_STATUS_TOO_LARGE."""
+        if int(max_stance) != getattr(self, "_hint", None):
+            _lib.check(self._ctx, self.lib.mpcqp_set_stance_hint(self._ctx, int(max_stance)), "set_stance_hint")
+            self._hint = int(max_stance)
 
     def __del__(self):
         ctx = getattr(self, "_ctx", None)

@@ -121,3 +121,63 @@ def test_shim_control_loop_matches_oracle():
             x, _, _ = Q.solve_qp_dual_active_set(o["H"], o["g"], o["C"], o["lb"], o["ub"])
             assert u0.shape == (12,)
             assert rel_err_u0(u0, x[:12]) < 1e-4
+
+
+def test_shim_rejects_non_diagonal_weights():
+    """mpc.py:50,52 build Qbar = kron(I_N, Q) from a full matrix; the engine's closed
+    form needs a diagonal Q / R, so an off-diagonal entry raises (never truncated)."""
+    m = _shim()
+
+    class OffDiagQ(LinearMpcConfig):
+        Q = LinearMpcConfig.Q.copy()
+    OffDiagQ.Q[0, 1] = OffDiagQ.Q[1, 0] = 0.5
+
+    class OffDiagR(LinearMpcConfig):
+        R = LinearMpcConfig.R.copy()
+    OffDiagR.R[3, 4] = 1e-6
+
+    with pytest.raises(ValueError, match="off-diagonal"):
+        m.ModelPredictiveController(OffDiagQ, AliengoConfig)
+    with pytest.raises(ValueError, match="off-diagonal"):
+        m.ModelPredictiveController(OffDiagR, AliengoConfig)
+    c = m.ModelPredictiveController(LinearMpcConfig, AliengoConfig)   # diagonal: accepted
+    np.testing.assert_array_equal(c.q_diag, np.diag(LinearMpcConfig.Q))
+
+
+class LinearMpcConfig16(LinearMpcConfig):   # the reference default: horizon = 16 (linear_mpc_configs.py:11)
+    horizon = 16
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("member", ["TROTTING10", "TROTTING16", "PACING10", "PACING16", "JUMPING16", "STANDING"])
+def test_shim_default_config_every_gait(member):
+    """Config 1 at the reference's defaults: Aliengo, LinearMpcConfig.horizon = 16, the
+    controller loop of scripts/mujoco_aliengo.py:184-207 over every Gait member
+    (gait.py:16-22; STANDING is n = 192, the interior-point class) -- the first-step
+    GRFs of each MPC tick against the oracle's exact optimum."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from helpers import rel_err_u0
+    from oracle import formulation as F
+    from oracle import qp as Q
+    from mpcqp.params import GAITS, GAIT_MEMBERS
+    from mpcqp.synthetic import gait_table
+    m = _shim()
+    c = m.ModelPredictiveController(LinearMpcConfig16, AliengoConfig)
+    rd = FakeRobotData(yaw=-0.4, vx=0.6)
+    g = GAIT_MEMBERS[member]
+    period = GAITS[g][0]
+    ticks = 0
+    for it in range(0, 61):
+        # Gait.set_iteration / get_gait_table (gait.py:76-100)
+        table = gait_table(g, (it // 20) % period, 16).reshape(-1)
+        c.update_robot_state(rd)
+        u0 = c.update_mpc_if_needed(it, np.array([1.2, 0.0, 0.0]), 0.1, table, solver="drake")
+        if it % 20 == 0:
+            o = F.formulate(c.current_state, c.ref_traj, table,
+                            [np.asarray(f) for f in rd.pos_base_feet], AliengoConfig.base_inertia_base,
+                            AliengoConfig.mass_base, 16)
+            x, _, _ = Q.solve_qp_dual_active_set(o["H"], o["g"], o["C"], o["lb"], o["ub"])
+            assert u0.shape == (12,)
+            assert rel_err_u0(u0, x[:12]) < 1e-4, (member, it)
+            ticks += 1
+    assert ticks == 4
