@@ -1,7 +1,10 @@
 """bench.py -- QP solves/sec of the MI355X batched MPC engine (BASELINE.json metric).
 
   python bench.py --gpus N --steps K --warmup W
-  (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL backend)
+  (N > 1: one rank per GPU over RCCL -- launched by torch.distributed.run, or, when
+  WORLD_SIZE is unset, by bench.py itself: the parent spawns the N ranks before any
+  HIP call and exits with their status)
+  python bench.py --config config1      # the drop-in controller's per-tick latency (B = 1)
 
 Workload (BASELINE.json configs[1]): per GPU B = 1024 A1 robots, trotting
 (trot10), horizon N = 10, synthetic seeded states; weak scaling
@@ -37,7 +40,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="config2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="config2", choices=sorted(CONFIGS) + ["config1"])
+    ap.add_argument("--standing-every", type=int, default=0,
+                    help="diagnostics: make every k-th robot stand (the interior-point class)")
+    ap.add_argument("--total", type=int, default=0, help="--rehearse-cpu: global robots (uneven shards)")
+    ap.add_argument("--rehearse-cpu", action="store_true",
+                    help="no GPU: rehearse the rank / shard / gather logic over gloo with a stand-in "
+                         "that zero-fills u0 (no solve, not a measurement)")
     ap.add_argument("--batch", type=int, default=0, help="override batch per GPU")
     ap.add_argument("--no-gather", action="store_true", help="skip the end-of-step u0 gather")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
@@ -184,8 +193,176 @@ def time_callers(eng, h, B, N, dev, stream, reps=20):
     return out
 
 
+def spawn_ranks(n):
+    """One child process per rank (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set), started
+    before this process makes any HIP call; returns the worst exit status."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
+
+
+def rehearse_cpu(args, world, rank, dist):
+    """The N > 1 rank logic on CPU tensors over gloo: every rank builds its shard of the
+    workload (seed = base + rank), a stand-in zero-fills u0 (NO solve, NOT a measurement),
+    the u0 all-gather runs, max-over-ranks timing, one JSON line from rank 0."""
+    import numpy as np
+    import torch
+    from mpcqp.dist import gather_u0
+    from mpcqp.synthetic import make_batch
+    Bpg, N, gaits, robots, tilt = CONFIGS[args.config if args.config in CONFIGS else "config2"]
+    if args.batch:
+        Bpg = args.batch
+    from mpcqp.dist import shard
+    total = args.total if args.total else world * Bpg   # --total: uneven contiguous shards
+    start, Bpg = shard(total, rank, world)
+    h = make_batch(Bpg, N, seed=1000 + rank, gaits=gaits, robots=robots, tilt_deg=tilt)
+    x0 = torch.as_tensor(h["x0"])
+    u0 = torch.empty((Bpg, 12), dtype=torch.float32)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    rows, gather_ok = 0, True
+    for _ in range(args.steps):
+        # stand-in for the HIP solve: each row carries its global robot index
+        u0.copy_(torch.arange(start, start + Bpg, dtype=torch.float32)[:, None].expand(Bpg, 12))
+        allu = gather_u0(u0, total=total) if world > 1 else u0
+        rows = int(allu.shape[0])
+        gather_ok &= bool(torch.equal(allu[:, 0], torch.arange(total, dtype=torch.float32)))
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tmax = torch.tensor([elapsed], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": "QP solves/sec (whole node), horizon=10 GRF QP, at 1/2/4/8 MI355X",
+                          "value": world * Bpg * args.steps / float(tmax.item()), "unit": "QP/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": 0, "rehearsal": True,
+                          "note": "gloo rehearsal on CPU tensors: stand-in solve (zero fill), not a measurement",
+                          "gathered_rows": rows, "gather_ok": gather_ok, "x0_rows": int(x0.shape[0]),
+                          "config": {"workload": f"{args.config}: {total} robots over {world} ranks",
+                                     "global_batch": total,
+                                     "parallelism": f"robot-sharded x{world} + gloo all-gather of u0"}}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+class _SyntheticRobotData:
+    """The RobotData fields the drop-in controller reads (mpc.py:65-79, :83), for an
+    Aliengo trotting forward (synthetic: no simulator in the loop)."""
+
+    def __init__(self, t):
+        import numpy as np
+        yaw = 0.2 * np.sin(0.5 * t)
+        self.pos_base = np.array([1.2 * t, 0.01 * np.sin(t), 0.38 + 0.01 * np.sin(7 * t)])
+        self.lin_vel_base = np.array([1.2, 0.01 * np.cos(t), 0.07 * np.cos(7 * t)])
+        self.ang_vel_base = np.array([0.05 * np.sin(3 * t), 0.03, 0.1 * np.cos(0.5 * t)])
+        h = yaw / 2
+        self.quat_base = np.array([np.cos(h), 0.0, 0.0, np.sin(h)])
+        c, s = np.cos(yaw), np.sin(yaw)
+        self.R_base = np.array([[c, -s, 0], [s, c, 0], [0, 0, 1.0]])
+        body = [(0.2399, 0.134), (0.2399, -0.134), (-0.2399, 0.134), (-0.2399, -0.134)]
+        self.pos_base_feet = [self.R_base @ np.array([x, y, -0.38]) for x, y in body]
+
+
+def bench_config1(args):
+    """Config 1: the drop-in ModelPredictiveController (pympc-quadruped_amd/linear_mpc/mpc.py)
+    in the control loop of scripts/mujoco_aliengo.py:184-207 at the reference defaults
+    (Aliengo, LinearMpcConfig.horizon = 16, Gait.TROTTING10, 1 kHz control, an MPC solve
+    every 20th iteration).  Reports the wall-clock latency of an MPC tick (state packing,
+    device planner, formulate + solve, the D2H of the forces: what a 1 kHz loop waits for)
+    and of the iterations between MPC ticks, next to the CPU restatement of the
+    reference's per-tick formulation + solve on the same states (1 core)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "pympc-quadruped_amd", "linear_mpc"))
+    import importlib
+    mpc = importlib.import_module("mpc")
+    from mpcqp.params import ROBOT_PRESETS
+    from mpcqp.synthetic import gait_table
+    from oracle import formulation as F
+
+    class LinearMpcConfig:   # config/linear_mpc_configs.py:4-24 (values)
+        dt_control = 0.001
+        iteration_between_mpc = 20
+        dt_mpc = 0.05
+        horizon = 16
+        gravity = 9.81
+        friction_coef = 0.7
+        Q = np.diag(F.Q_DIAG)
+        R = np.diag(F.R_DIAG)
+
+    al = F.ROBOTS["aliengo"]
+
+    class AliengoConfig:     # config/robot_configs.py:44-60 (values)
+        mass_base = al["mass"]
+        base_height_des = al["height"]
+        base_inertia_base = al["inertia"]
+        fz_max = al["fz_max"]
+
+    N = LinearMpcConfig.horizon
+    ctl = mpc.ModelPredictiveController(LinearMpcConfig, AliengoConfig)
+    n_iter = (args.warmup + args.steps) * LinearMpcConfig.iteration_between_mpc
+    mpc_ms, other_ms, states = [], [], []
+    v_des = np.array([1.2, 0.0, 0.0])
+    for it in range(n_iter):
+        rd = _SyntheticRobotData(it * 1e-3)
+        table = gait_table("trot10", (it // 20) % 10, N).reshape(-1)
+        t0 = time.perf_counter()
+        ctl.update_robot_state(rd)
+        u = ctl.update_mpc_if_needed(it, v_des, 0.0, table, solver="drake")
+        dt = (time.perf_counter() - t0) * 1e3
+        if it >= args.warmup * 20:
+            if it % 20 == 0:
+                mpc_ms.append(dt)
+                if len(states) < 64:
+                    states.append((ctl.current_state.copy(), ctl.ref_traj.copy(), table.copy(),
+                                   [np.asarray(f) for f in rd.pos_base_feet]))
+            else:
+                other_ms.append(dt)
+    assert np.all(np.isfinite(u))
+    cpu = None
+    if not args.no_cpu:
+        from oracle import qp as Q
+        t0 = time.perf_counter()
+        done = 0
+        while time.perf_counter() - t0 < args.cpu_seconds and done < 10 * len(states):
+            x0, xr, tb, feet = states[done % len(states)]
+            o = F.formulate(x0, xr, tb, feet, al["inertia"], al["mass"], N)
+            Q.solve_qp_dual_active_set(o["H"], o["g"], o["C"], o["lb"], o["ub"])
+            done += 1
+        cpu = {"value": (time.perf_counter() - t0) / done * 1e3, "unit": "ms/tick", "cores": 1, "kind": "port",
+               "sample": f"{done} MPC ticks of the same run's states ({_cpu_model()}): reference-faithful NumPy "
+                         "formulation (oracle/formulation.py) + exact float64 dual active set (oracle/qp.py)"}
+    med = float(np.median(mpc_ms))
+    print(json.dumps({
+        "metric": "drop-in MPC tick latency (B=1, Aliengo, horizon 16, trot10)",
+        "value": med, "unit": "ms", "n_gpus": 1, "steps": len(mpc_ms), "warmup": args.warmup,
+        "higher_is_better": False, "dtype": "f64", "data": "synthetic Aliengo trot states (no simulator)",
+        "config": {"workload": "config1: ModelPredictiveController drop-in, scripts/mujoco_aliengo.py loop, "
+                               "LinearMpcConfig.horizon = 16, Gait.TROTTING10", "batch": 1, "horizon": N},
+        "mpc_tick_ms": {"median": med, "p90": float(np.percentile(mpc_ms, 90)), "mean": float(np.mean(mpc_ms))},
+        "other_tick_ms": {"median": float(np.median(other_ms)), "p90": float(np.percentile(other_ms, 90))},
+        "cpu_baseline": cpu,
+    }))
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+    if args.config == "config1":
+        return bench_config1(args)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -198,6 +375,11 @@ def main():
     # one rank per GPU; ranks beyond the visible devices wrap around (only a rehearsal
     # of the N > 1 path on a smaller box does that).  MPCQP_BENCH_BACKEND=gloo is for
     # such rehearsals too: the measured path is "nccl" (RCCL over xGMI).
+    if args.rehearse_cpu:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+        return rehearse_cpu(args, world, rank, dist)
     local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -220,6 +402,9 @@ def main():
     nbat = 4
     host = [make_batch(Bpg, N, seed=1000 * (k + 1) + rank, gaits=gaits, robots=robots, tilt_deg=tilt)
             for k in range(nbat)]
+    if args.standing_every:
+        for h in host:
+            h["contact"][::args.standing_every] = 1.0
     # the caller knows its contact schedules: promise the largest stance count so the
     # engine launches only the capacity classes the workload can reach
     max_stance = int(max((h["contact"] > 0).reshape(Bpg, -1).sum(1).max() for h in host))
@@ -229,20 +414,28 @@ def main():
     for h in host:
         dev_b.append({k: torch.as_tensor(v).to(dev).contiguous() for k, v in h.items()})
     u0 = torch.empty((Bpg, 12), dtype=torch.float32, device=dev)
-    status = torch.empty((Bpg,), dtype=torch.int32, device=dev)
+    status = [torch.empty((Bpg,), dtype=torch.int32, device=dev) for _ in range(nbat)]
     iters = [torch.empty((Bpg,), dtype=torch.int32, device=dev) for _ in range(nbat)]
     stream = torch.cuda.current_stream(dev)
+    gather_events = []
 
     def step(k, ev=None):
         d = dev_b[k % nbat]
         if ev is not None:
             ev[0].record(stream)
         eng.solve_raw(Bpg, d["x0"], d["xref"], d["contact"], d["feet"], d["robot"], u0,
-                      None, status, iters[k % nbat], stream=stream)
+                      None, status[k % nbat], iters[k % nbat], stream=stream)
         if ev is not None:
             ev[1].record(stream)
         if world > 1 and not args.no_gather:
-            gather_u0(u0)
+            if ev is not None:   # the RCCL all-gather, timed on its own
+                g = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                g[0].record(stream)
+                gather_u0(u0)
+                g[1].record(stream)
+                gather_events.append(g)
+            else:
+                gather_u0(u0)
 
     for k in range(args.warmup):
         step(k)
@@ -290,7 +483,7 @@ def main():
         flops_launch.append(sum(algorithmic_flops(N, int(n), int(i)) for n, i in zip(ns, it)))
         exec_launch.append(sum(executed_flops(N, int(n), int(i)) for n, i in zip(ns, it)))
         it_all.append(it)
-    st = status.cpu().numpy()
+    st = np.concatenate([x.cpu().numpy() for x in status])   # every batch's last solve
     steps_per_bat = [sum(1 for s in range(args.steps) if s % nbat == k) for k in range(nbat)]
     F_avg = sum(f * c for f, c in zip(flops_launch, steps_per_bat)) / args.steps
     E_avg = sum(f * c for f, c in zip(exec_launch, steps_per_bat)) / args.steps
@@ -310,6 +503,8 @@ def main():
         traffic = None
 
     callers = None if args.no_callers else time_callers(eng, host[0], Bpg, N, dev, stream)
+    gather_ms = (sum(a.elapsed_time(b) for a, b in gather_events) / len(gather_events)
+                 if gather_events else None)
 
     gather_label = ""
     if world > 1 and not args.no_gather:
@@ -344,8 +539,11 @@ def main():
                                    f"robots {'+'.join(robots)}" + (f", cone tilt <= {tilt} deg" if tilt else ""),
                        "batch_per_gpu": Bpg, "horizon": N, "global_batch": world * Bpg,
                        "parallelism": f"robot-sharded x{world}" + gather_label},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP64_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic},
+            # the governing pipe is the FP64 vector ALU (VALU): no MFMA instruction is on
+            # the path (gfx950's FP64 MFMA peak equals its FP64 VALU peak)
+            "roofline": {"bound": "valu", "pipe": "fp64 VALU", "achieved": achieved, "peak": PEAK_FP64_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic,
+                         "executed_frac": E_avg / kavg_s / 1e12 / PEAK_FP64_TFLOPS},
             "cpu_baseline": cpu,
             "kernel_ms_avg": kavg_s * 1e3,
             "executed_tflops": E_avg / kavg_s / 1e12,
@@ -354,6 +552,10 @@ def main():
             "status_ok_frac": float((st == 0).mean()),
             "callers": callers,
         }
+        if gather_ms is not None:
+            line["gather_ms_avg"] = gather_ms
+        if args.standing_every:
+            line["config"]["workload"] += f", every {args.standing_every}th robot standing"
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

@@ -47,3 +47,25 @@ def test_gather_u0_world2(total):
         assert p.exitcode == 0
     for r in range(world):
         assert res[r] == [float(i) for i in range(total)]
+
+
+@pytest.mark.parametrize("total", [2048, 7])
+def test_bench_spawns_its_own_ranks(total):
+    """`python bench.py --gpus 2` with no WORLD_SIZE spawns the two ranks itself (the
+    parent makes no HIP call); --rehearse-cpu runs the rank logic over gloo on CPU
+    tensors -- shard, stand-in solve, u0 all-gather (uneven shards for 7 robots),
+    max-over-ranks timing -- and rank 0 prints one line with n_gpus = 2."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--rehearse-cpu",
+                          "--steps", "3", "--total", str(total)],
+                         capture_output=True, text=True, timeout=300, env=env, check=True)
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout   # rank 0 only
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["rehearsal"] is True
+    assert line["gathered_rows"] == total and line["gather_ok"] is True
+    assert line["config"]["global_batch"] == total
