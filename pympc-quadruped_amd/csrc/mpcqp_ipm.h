@@ -39,7 +39,8 @@ constexpr double IPM_TAU = 0.995;
 constexpr double IPM_POLISH_MU = 1e-7;
 constexpr double IPM_MU_FLOOR = 1e-13;
 constexpr double IPM_STAT_TOL = 1e-10;
-constexpr int IPM_FPL = 2;   // stance foot-steps per lane (4 kMaxN <= 128)
+constexpr int IPM_FPL = 2;             // stance foot-steps per lane (4 kMaxN <= 128)
+constexpr int IPM_NF = 4 * kMaxN;
 
 struct alignas(16) IpmShared {
   union {
@@ -47,29 +48,81 @@ struct alignas(16) IpmShared {
       Form f;
       FormY fy;
     } fa;                          // formulation scratch (dead once Bm / x0 / xr are copied)
-    double S[kMaxN][144];          // Riccati S_k (12 x 12, row-major)
+    alignas(16) double S[kMaxN][144];   // Riccati S_k (12 x 12, row-major, symmetric)
   };
   RobotMeta mt;
-  double Bm[12][12];               // B_d rows 0..11 (row 12 is 0)
+  alignas(16) double Bm[12][12];   // B_d rows 0..11 (row 12 is 0)
+  alignas(16) double BmT[12][12];  // its transpose
+  union {
+    alignas(16) double CW[12][12];   // factor scratch: B blockdiag(W) (dead once E is formed)
+    alignas(16) double TT[12][12];   // factor scratch: (I + P E)^T, then S_k^T
+  };
+  alignas(16) double E[12][12];    // factor scratch: E_k, then S_k A
   double nmr[3][3];                // h R_z^T: A_d[r][6 + c] (r < 3)
   double x0[16];
   double xr[kMaxN][NX];            // xref, float64
   double qh[16];                   // 2 q
   double rh[NU];                   // 2 r
-  double W[4 * kMaxN][9];          // per stance foot-step 3x3 weight
-  double E[144];
-  double M[12][24];                // Gauss-Jordan [I + P E | P]
-  double P[144];
-  double U[kMaxN][NU];             // iterate (swing entries 0)
-  double dU[kMaxN][NU];
-  double rhs[kMaxN][NU];
-  double gr[kMaxN][NU];
-  double Y[kMaxN][NU];
-  double By[kMaxN][NU];
-  double Us[kMaxN][NU];            // the IPM iterate while a polish overwrites U
-  double X[kMaxN + 1][16];
-  double v0[16], v1[16], v2[16], vn[2][16];
+  double W[IPM_NF][9];             // per stance foot-step 3x3 weight of the Newton system
+  alignas(16) double P[144];       // P_{k+1}
+  alignas(16) double U[kMaxN][NU]; // iterate (swing entries 0)
+  alignas(16) double dU[kMaxN][NU];
+  alignas(16) double rhs[kMaxN][NU];
+  alignas(16) double gr[kMaxN][NU];
+  alignas(16) double Y[kMaxN][NU];
+  alignas(16) double By[kMaxN][NU];
+  alignas(16) double Us[kMaxN][NU];   // the IPM iterate while a polish overwrites U
+  alignas(16) double X[kMaxN + 1][16];
+  alignas(16) double nu[2][16];
+  alignas(16) double pv[2][16];
+  alignas(16) double dx[2][16];
+  alignas(16) double w[16];
+  // per stance foot-step interior-point state (row slots 0..5)
+  double fs[IPM_NF][6], fl[IPM_NF][6], frp[IPM_NF][6], frd[IPM_NF][4];
+  union {
+    struct {
+      double fds[IPM_NF][6], fdl[IPM_NF][6];   // Newton directions of s and lambda
+    };
+    double fpj[IPM_NF][9];         // polish: null-space projector per foot-step
+  };
+  int fact[IPM_NF];                // polish: active rows per foot-step
+  int fprev[IPM_NF];               // polish: the rows of the previous try
 };
+
+// 12 / 16 consecutive doubles of a 16-B aligned LDS vector, 16 B per read
+__device__ __forceinline__ void ld12(double (&v)[12], const double* p) {
+  const d2* q = reinterpret_cast<const d2*>(p);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const d2 x = q[i];
+    v[2 * i] = x[0];
+    v[2 * i + 1] = x[1];
+  }
+}
+__device__ __forceinline__ void ld16(double (&v)[16], const double* p) {
+  const d2* q = reinterpret_cast<const d2*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const d2 x = q[i];
+    v[2 * i] = x[0];
+    v[2 * i + 1] = x[1];
+  }
+}
+__device__ __forceinline__ void st12(double* p, const double (&v)[12]) {
+  d2* q = reinterpret_cast<d2*>(p);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) q[i] = d2{v[2 * i], v[2 * i + 1]};
+}
+__device__ __forceinline__ double dot12(const double (&a)[12], const double (&b)[12]) {
+  double s0 = a[0] * b[0], s1 = a[1] * b[1], s2 = a[2] * b[2];
+#pragma unroll
+  for (int i = 3; i < 12; i += 3) {
+    s0 = fma(a[i], b[i], s0);
+    s1 = fma(a[i + 1], b[i + 1], s1);
+    s2 = fma(a[i + 2], b[i + 2], s2);
+  }
+  return (s0 + s1) + s2;
+}
 
 __device__ __forceinline__ double wave_sum_d(double v) {
   v += dpp_d<DPP_XOR1>(v);
@@ -86,16 +139,14 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   }
   return readlane_d(v, 63);
 }
-__device__ __forceinline__ double wave_min_all(double v) { return wave_min(v); }
-__device__ __forceinline__ double wave_max_all(double v) { return wave_max_d(v); }
 
-
-// One robot with n > 126 stance variables.  Called by a 64-thread workgroup.
-__device__ void solve_robot_ipm(const KParams& KP, int b, IpmShared& sm, const float* __restrict__ x0g,
-                                const float* __restrict__ xrefg, const float* __restrict__ contactg,
-                                const float* __restrict__ feetg, const float* __restrict__ robotg,
-                                float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg,
-                                int* __restrict__ itersg) {
+// One robot with more than 128 stance variables.  Called by a 64-thread workgroup.
+__device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmShared& sm,
+                                                const float* __restrict__ x0g, const float* __restrict__ xrefg,
+                                                const float* __restrict__ contactg, const float* __restrict__ feetg,
+                                                const float* __restrict__ robotg, float* __restrict__ u0g,
+                                                float* __restrict__ Ug, int* __restrict__ statusg,
+                                                int* __restrict__ itersg) {
   constexpr int NT = LANES;
   const int lane = threadIdx.x;
   const int N = KP.N;
@@ -122,6 +173,7 @@ __device__ void solve_robot_ipm(const KParams& KP, int b, IpmShared& sm, const f
       else if (i < 9) v = smf.K[i - 6][c] * h;
       else v = (c % 3 == i - 9) ? h * minv : 0.0;
       sm.Bm[i][c] = v;
+      sm.BmT[c][i] = v;
     }
     if (lane < 9) {
       const int r = lane / 3, c = lane % 3;   // (R_z^T)[r][c] = R_z[c][r]
@@ -140,303 +192,319 @@ __device__ void solve_robot_ipm(const KParams& KP, int b, IpmShared& sm, const f
   fsync<NT>();   // the formulation scratch (union with S) is dead from here on
 
   // ------------------------------------------------ per-lane foot-steps
-  const bool implied = sm.mt.fz0_implied != 0;
-  int jt[IPM_FPL], jl[IPM_FPL];
-  bool own[IPM_FPL];
-  double hb[IPM_FPL];   // h of row 5: -ub
-#pragma unroll
-  for (int q = 0; q < IPM_FPL; ++q) {
-    const int j = lane + LANES * q;
-    own[q] = j < S;
-    jt[q] = own[q] ? sm.mt.foot_t[j] : 0;
-    jl[q] = own[q] ? sm.mt.foot_leg[j] : 0;
-    hb[q] = own[q] ? -sm.mt.ub[j] : 0.0;
-  }
-  auto live = [&](int r) -> bool { return r != 4 || !implied; };
-  auto arow = [&](int r, int k) -> double { return sm.mt.rows[r][k]; };
-  auto hrow = [&](int q, int r) -> double { return r == 5 ? hb[q] : 0.0; };
-  const int R = implied ? 5 : 6;
+  const int liv = sm.mt.fz0_implied != 0 ? 0x2F : 0x3F;   // live rows: n.f >= 0 is implied when mu > 0
+  const int R = sm.mt.fz0_implied != 0 ? 5 : 6;
   const double m_tot = (double)(S * R);
+  double rw[6][3];   // cone rows (wave-uniform)
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int x = 0; x < 3; ++x) rw[r][x] = sgpr_d(sm.mt.rows[r][x]);
+  auto adot = [&](int r, const double (&v)[3]) -> double {
+    return rw[r][0] * v[0] + rw[r][1] * v[1] + rw[r][2] * v[2];
+  };
+  auto foot = [&](int j, const double (*A)[NU], double (&o)[3]) {   // stance foot-step j of an N x 12 array
+    const double* p = &A[sm.mt.foot_t[j]][3 * sm.mt.foot_leg[j]];
+    o[0] = p[0];
+    o[1] = p[1];
+    o[2] = p[2];
+  };
+  auto foot_ptr = [&](int j, double (*A)[NU]) -> double* { return &A[sm.mt.foot_t[j]][3 * sm.mt.foot_leg[j]]; };
+  auto legrh = [&](int j, double (&o)[3]) {
+    const int l = sm.mt.foot_leg[j];
+    o[0] = sm.rh[3 * l];
+    o[1] = sm.rh[3 * l + 1];
+    o[2] = sm.rh[3 * l + 2];
+  };
 
-  // ------------------------------------------------ stage recursions
-  // Nm = A_d - I on the 13-state: rows 0..2 <- h R_z^T x[6..8]; rows 3..5 <- h x[9..11]
-  // (+ h^2/2 x[12] on row 5); row 11 <- h x[12]
-  auto gradient = [&]() {   // sm.gr = H U + g on stance coordinates (forward sim + adjoint)
+#ifdef MPCQP_IPM_DEBUG
+  unsigned long long cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, cyc_t0 = __builtin_amdgcn_s_memtime();
+#define IPM_T0() const unsigned long long t0_ = __builtin_amdgcn_s_memtime()
+#define IPM_T1(i) cyc[i] += __builtin_amdgcn_s_memtime() - t0_
+#define IPM_TS(v)                                                   \
+  __builtin_amdgcn_sched_barrier(0);                                \
+  const unsigned long long v = __builtin_amdgcn_s_memtime();        \
+  __builtin_amdgcn_sched_barrier(0)
+#define IPM_TA(i, a, bb) cyc[i] += (bb) - (a)
+#else
+#define IPM_TS(v) do {} while (0)
+#define IPM_TA(i, a, bb) do {} while (0)
+#define IPM_T0() do {} while (0)
+#define IPM_T1(i) do {} while (0)
+#endif
+  // ------------------------------------------------ stage recursions (one wave; LDS
+  // phases separated by fsync).  Nm = A_d - I on the 13-state: rows 0..2 <- h R_z^T
+  // x[6..8]; rows 3..5 <- h x[9..11] (+ h^2/2 x[12] on row 5); row 11 <- h x[12].
+  // sm.gr = H U + g on stance coordinates: forward simulation + adjoint recursion
+  // Every stage phase loads its operands as whole 12-vectors (6 x 16-B LDS reads issued
+  // back to back) and keeps the lane's own rows of B_d in registers: one LDS round trip
+  // per phase instead of one per product term.
+  auto gradient = [&]() {
+    IPM_T0();
+    double brow[12], bcol[12];   // row `lane` of B_d (lanes < 12); column lane - 32 (lanes 32..43)
+    if (lane < 12) ld12(brow, sm.Bm[lane]);
+    if (lane >= 32 && lane < 44) ld12(bcol, sm.BmT[lane - 32]);
     if (lane < NX) sm.X[0][lane] = sm.x0[lane];
     fsync<NT>();
     for (int k = 0; k < N; ++k) {
       if (lane < NX) {
-        const double* x = sm.X[k];
+        double x[16], u[12];
+        ld16(x, sm.X[k]);
+        ld12(u, sm.U[k]);
         double v = x[lane];
         if (lane < 3) v += sm.nmr[lane][0] * x[6] + sm.nmr[lane][1] * x[7] + sm.nmr[lane][2] * x[8];
         else if (lane < 6) v += h * x[lane + 6] + (lane == 5 ? 0.5 * h * h * x[12] : 0.0);
         else if (lane == 11) v += h * x[12];
-        if (lane < 12) {
-#pragma unroll
-          for (int c = 0; c < NU; ++c) v = fma(sm.Bm[lane][c], sm.U[k][c], v);
-        }
+        if (lane < 12) v += dot12(brow, u);
         sm.X[k + 1][lane] = v;
       }
       fsync<NT>();
     }
-    for (int k = N - 1; k >= 0; --k) {
-      double* nu = sm.vn[k & 1];
-      const double* np = sm.vn[(k + 1) & 1];
-      if (lane < NX) {
+    // phase k: lanes 0..12 form nu_k from nu_{k+1}; lanes 32..43 the gradient of stage k + 1
+    for (int k = N - 1; k >= -1; --k) {
+      double np[16];
+      ld16(np, sm.nu[(k + 1) & 1]);
+      if (k >= 0 && lane < NX) {
         double v = sm.qh[lane] * (sm.X[k + 1][lane] - sm.xr[k][lane]);
         if (k < N - 1) {
-          double a = np[lane];
-          if (lane >= 6 && lane < 9)
-            a += sm.nmr[0][lane - 6] * np[0] + sm.nmr[1][lane - 6] * np[1] + sm.nmr[2][lane - 6] * np[2];
-          else if (lane >= 9 && lane < 12) a += h * np[lane - 6];
+          double a = np[lane & 15];
+          if (lane >= 6 && lane < 9) a += sm.nmr[0][lane - 6] * np[0] + sm.nmr[1][lane - 6] * np[1] + sm.nmr[2][lane - 6] * np[2];
+          else if (lane >= 9 && lane < 12) a += h * np[(lane - 6) & 15];
           else if (lane == 12) a += 0.5 * h * h * np[5] + h * np[11];
           v += a;
         }
-        nu[lane] = v;
+        sm.nu[k & 1][lane] = v;
+      }
+      if (k + 1 < N && lane >= 32 && lane < 32 + NU) {
+        const int c = lane - 32, kk = k + 1;
+        const bool st = sm.mt.stance_of[4 * kk + c / 3] >= 0;
+        double nv[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) nv[i] = np[i];
+        const double g = sm.rh[c] * sm.U[kk][c] + dot12(bcol, nv);
+        sm.gr[kk][c] = st ? g : 0.0;
       }
       fsync<NT>();
-      if (lane < NU) {
-        const bool st = sm.mt.stance_of[4 * k + lane / 3] >= 0;
-        double g = sm.rh[lane] * sm.U[k][lane];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) g = fma(sm.Bm[i][lane], nu[i], g);
-        sm.gr[k][lane] = st ? g : 0.0;
-      }
     }
-    fsync<NT>();
+    IPM_T1(0);
   };
 
-  // (A^T v)[i] on the 12-state, v in LDS
-  auto at_apply = [&](const double* v, int i) -> double {
-    double a = v[i];
-    if (i >= 6 && i < 9) a += sm.nmr[0][i - 6] * v[0] + sm.nmr[1][i - 6] * v[1] + sm.nmr[2][i - 6] * v[2];
-    else if (i >= 9) a += h * v[i - 6];
-    return a;
-  };
-  // (A v)[i] on the 12-state
-  auto a_apply = [&](const double* v, int i) -> double {
-    double a = v[i];
-    if (i < 3) a += sm.nmr[i][0] * v[6] + sm.nmr[i][1] * v[7] + sm.nmr[i][2] * v[8];
-    else if (i < 6) a += h * v[i + 6];
-    return a;
-  };
-
-  // Riccati factorisation with the per-foot-step weights sm.W: S_k for every stage
+  // Riccati factorisation with the per-foot-step weights sm.W: S_k for every stage.
+  // Per stage (P = P_{k+1} symmetric): CW = B blockdiag(W) (entry (m, c) = W_leg(c) row .
+  // B[m][leg(c)]), E = B CW^T (symmetric), T^T = (I + P E)^T; lane j < 12 holds column j
+  // of T and lane 12 + j column j of P in registers for the Gauss-Jordan sweep on [T | P]
+  // (pivot column broadcast by readlane); S_k = T^-1 P symmetrised; P_k = Qh + A^T S_k A.
   auto factor = [&]() {
+    IPM_T0();
     for (int e = lane; e < 144; e += NT) sm.P[e] = (e / 12 == e % 12) ? sm.qh[e / 12] : 0.0;
     fsync<NT>();
+    const int jc = lane < 12 ? lane : (lane < 24 ? lane - 12 : 0);
     for (int k = N - 1; k >= 0; --k) {
-      // E_k = sum_legs B_leg W B_leg^T
-      for (int e = lane; e < 144; e += NT) {
-        const int i = e / 12, m = e % 12;
-        double v = 0.0;
+      IPM_TS(ta);
+      // CW[m][c] (zero columns for swing legs)
 #pragma unroll
-        for (int l = 0; l < 4; ++l) {
+      for (int t = 0; t < 3; ++t) {
+        const int e = lane + NT * t;
+        if (e < 144) {
+          const int m = e / 12, c = e % 12, l = c / 3, a = c % 3;
           const int j = sm.mt.stance_of[4 * k + l];
+          double v = 0.0;
           if (j >= 0) {
-            const double* w = sm.W[j];
-            const double* bi = &sm.Bm[i][3 * l];
-            const double* bm = &sm.Bm[m][3 * l];
-#pragma unroll
-            for (int a = 0; a < 3; ++a) v = fma(bi[a], w[3 * a] * bm[0] + w[3 * a + 1] * bm[1] + w[3 * a + 2] * bm[2], v);
+            const double* wr = sm.W[j] + 3 * a;
+            v = wr[0] * sm.Bm[m][3 * l] + wr[1] * sm.Bm[m][3 * l + 1] + wr[2] * sm.Bm[m][3 * l + 2];
           }
+          sm.CW[m][c] = v;
         }
-        sm.E[e] = v;
       }
       fsync<NT>();
-      // [I + P E | P]
-      double tv[3];
+      // E[i][m] = B row i . CW row m
 #pragma unroll
       for (int t = 0; t < 3; ++t) {
         const int e = lane + NT * t;
-        tv[t] = 0.0;
+        if (e < 144) {
+          const int i = e / 12, m = e % 12;
+          double bi[12], cm[12];
+          ld12(bi, sm.Bm[i]);
+          ld12(cm, sm.CW[m]);
+          sm.E[i][m] = dot12(bi, cm);
+        }
+      }
+      fsync<NT>();
+      // T[i][j] = delta + P row i . E row j (E symmetric), stored transposed
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int e = lane + NT * t;
         if (e < 144) {
           const int i = e / 12, j = e % 12;
-          double v = (i == j) ? 1.0 : 0.0;
-#pragma unroll
-          for (int m = 0; m < 12; ++m) v = fma(sm.P[12 * i + m], sm.E[12 * m + j], v);
-          tv[t] = v;
-        }
-      }
-#pragma unroll
-      for (int t = 0; t < 3; ++t) {
-        const int e = lane + NT * t;
-        if (e < 144) {
-          sm.M[e / 12][e % 12] = tv[t];
-          sm.M[e / 12][12 + e % 12] = sm.P[e];
+          double pi[12], ej[12];
+          ld12(pi, sm.P + 12 * i);
+          ld12(ej, sm.E[j]);
+          sm.TT[j][i] = dot12(pi, ej) + (i == j ? 1.0 : 0.0);
         }
       }
       fsync<NT>();
-      // Gauss-Jordan: right half becomes (I + P E)^-1 P
+      IPM_TS(tb);
+      double col[12];
+      if (lane < 12) ld12(col, sm.TT[jc]);
+      else ld12(col, sm.P + 12 * jc);   // column jc of P = row jc (P symmetric)
+#pragma unroll
       for (int kk = 0; kk < 12; ++kk) {
-        const double ip = 1.0 / sm.M[kk][kk];
-        double nv[5];
+        double pc[12];
 #pragma unroll
-        for (int t = 0; t < 5; ++t) {
-          const int e = lane + NT * t;
-          const int i = e / 24, j = e % 24;
-          nv[t] = 0.0;
-          if (e < 288 && j > kk) {
-            const double rowv = sm.M[kk][j] * ip;
-            nv[t] = (i == kk) ? rowv : fma(-sm.M[i][kk], rowv, sm.M[i][j]);
-          }
-        }
+        for (int i = 0; i < 12; ++i) pc[i] = readlane_d(col[i], kk);
+        const double ip = rcp_nr(pc[kk]);
+        const double rowv = col[kk] * ip;
 #pragma unroll
-        for (int t = 0; t < 5; ++t) {
-          const int e = lane + NT * t;
-          const int i = e / 24, j = e % 24;
-          if (e < 288 && j > kk) sm.M[i][j] = nv[t];
-        }
-        fsync<NT>();
+        for (int i = 0; i < 12; ++i) col[i] = (i == kk) ? rowv : fma(-pc[i], rowv, col[i]);
       }
-      for (int e = lane; e < 144; e += NT) {
-        const int i = e / 12, j = e % 12;
-        sm.S[k][e] = 0.5 * (sm.M[i][12 + j] + sm.M[j][12 + i]);
+      IPM_TS(tc);
+      if (lane >= 12 && lane < 24) st12(sm.TT[jc], col);   // S^T row jc = column jc of S
+      fsync<NT>();
+      IPM_TS(td);
+      IPM_TA(4, ta, tb);
+      IPM_TA(5, tb, tc);
+      IPM_TA(6, tc, td);
+      // S_k = (S + S^T) / 2 (sm.TT holds S^T); S_k A into sm.E
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int e = lane + NT * t;
+        if (e < 144) {
+          const int i = e / 12, j = e % 12;
+          auto ss = [&](int m, int n) -> double { return 0.5 * (sm.TT[m][n] + sm.TT[n][m]); };
+          double v = ss(i, j);
+          sm.S[k][e] = v;
+          if (j >= 6 && j < 9) v += ss(i, 0) * sm.nmr[0][j - 6] + ss(i, 1) * sm.nmr[1][j - 6] + ss(i, 2) * sm.nmr[2][j - 6];
+          else if (j >= 9) v += h * ss(i, j - 6);
+          sm.E[i][j] = v;
+        }
       }
       fsync<NT>();
-      if (k > 0) {
-        // P_k = Qh + A^T S_k A  (A = I + Nm on the 12-state)
-        const double* Sk = sm.S[k];
-        for (int e = lane; e < 144; e += NT) {
-          const int i = e / 12, j = e % 12;
-          // (S A)[m][j] for the rows m that column i of Nm touches, and S[i][.] A[.][j]
-          auto sa = [&](int m) -> double {   // (S_k A)[m][j]
-            double v = Sk[12 * m + j];
-            if (j >= 6 && j < 9) v += Sk[12 * m + 0] * sm.nmr[0][j - 6] + Sk[12 * m + 1] * sm.nmr[1][j - 6] +
-                                      Sk[12 * m + 2] * sm.nmr[2][j - 6];
-            else if (j >= 9) v += h * Sk[12 * m + j - 6];
-            return v;
-          };
-          double v = sa(i);
-          if (i >= 6 && i < 9) v += sm.nmr[0][i - 6] * sa(0) + sm.nmr[1][i - 6] * sa(1) + sm.nmr[2][i - 6] * sa(2);
-          else if (i >= 9) v += h * sa(i - 6);
-          if (i == j) v += sm.qh[i];
-          sm.P[e] = v;
+      IPM_TS(te);
+      IPM_TA(7, td, te);
+      if (k > 0) {   // P_k = Qh + A^T (S_k A)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          const int e = lane + NT * t;
+          if (e < 144) {
+            const int i = e / 12, j = e % 12;
+            double v = sm.E[i][j];
+            if (i >= 6 && i < 9) v += sm.nmr[0][i - 6] * sm.E[0][j] + sm.nmr[1][i - 6] * sm.E[1][j] + sm.nmr[2][i - 6] * sm.E[2][j];
+            else if (i >= 9) v += h * sm.E[i - 6][j];
+            if (i == j) v += sm.qh[i];
+            sm.P[e] = v;
+          }
         }
         fsync<NT>();
       }
     }
+    IPM_T1(1);
   };
 
-  // (H + G^T D G) d = rhs restricted to the foot-steps' subspaces (sm.rhs -> sm.dU)
+  // (H + G^T D G) d = rhs restricted to the foot-steps' subspaces: sm.rhs -> sm.dU
   auto lsolve = [&]() {
-    if (lane < 12) sm.v0[lane] = 0.0;
+    IPM_T0();
+    // lanes c < 12: the three B_d columns of the lane's leg and B_d row c
+    double bl0[12], bl1[12], bl2[12], brow[12];
+    if (lane < 12) {
+      const int l = lane / 3;
+      ld12(bl0, sm.BmT[3 * l]);
+      ld12(bl1, sm.BmT[3 * l + 1]);
+      ld12(bl2, sm.BmT[3 * l + 2]);
+      ld12(brow, sm.Bm[lane]);
+    }
+    if (lane < 16) sm.pv[0][lane] = 0.0;
     fsync<NT>();
+    int pb = 0;
     for (int k = N - 1; k >= 0; --k) {
-      if (lane < NU) {
-        const int j = sm.mt.stance_of[4 * k + lane / 3];
-        double z = 0.0;
-        if (j >= 0) {
-          z = -sm.rhs[k][lane];
-#pragma unroll
-          for (int i = 0; i < 12; ++i) z = fma(sm.Bm[i][lane], sm.v0[i], z);
-        }
-        sm.v1[lane] = z;
-      }
-      fsync<NT>();
-      if (lane < NU) {
+      if (lane < NU) {   // Y = W (B_leg^T p - rhs_leg) for the lane's leg
         const int l = lane / 3, a = lane % 3;
         const int j = sm.mt.stance_of[4 * k + l];
         double y = 0.0;
         if (j >= 0) {
-          const double* w = sm.W[j] + 3 * a;
-          y = w[0] * sm.v1[3 * l] + w[1] * sm.v1[3 * l + 1] + w[2] * sm.v1[3 * l + 2];
+          double p[12];
+          ld12(p, sm.pv[pb]);
+          const double z0 = dot12(bl0, p) - sm.rhs[k][3 * l];
+          const double z1 = dot12(bl1, p) - sm.rhs[k][3 * l + 1];
+          const double z2 = dot12(bl2, p) - sm.rhs[k][3 * l + 2];
+          const double* wj = sm.W[j] + 3 * a;
+          y = wj[0] * z0 + wj[1] * z1 + wj[2] * z2;
         }
         sm.Y[k][lane] = y;
       }
       fsync<NT>();
       if (lane < 12) {
-        double v = 0.0;
-#pragma unroll
-        for (int c = 0; c < NU; ++c) v = fma(sm.Bm[lane][c], sm.Y[k][c], v);
-        sm.By[k][lane] = v;
+        double y[12];
+        ld12(y, sm.Y[k]);
+        sm.By[k][lane] = dot12(brow, y);
       }
       fsync<NT>();
-      if (k > 0) {
+      if (k > 0) {   // p <- A^T (p - S_k By)
         if (lane < 12) {
-          double t = sm.v0[lane];
-#pragma unroll
-          for (int m = 0; m < 12; ++m) t = fma(-sm.S[k][12 * lane + m], sm.By[k][m], t);
-          sm.v2[lane] = t;
+          double by[12], sr[12];
+          ld12(by, sm.By[k]);
+          const double* p = sm.pv[pb];
+          auto tt = [&](int m) -> double {
+            ld12(sr, sm.S[k] + 12 * m);
+            return p[m] - dot12(sr, by);
+          };
+          double v = tt(lane);
+          if (lane >= 6 && lane < 9) v += sm.nmr[0][lane - 6] * tt(0) + sm.nmr[1][lane - 6] * tt(1) + sm.nmr[2][lane - 6] * tt(2);
+          else if (lane >= 9) v += h * tt(lane - 6);
+          sm.pv[pb ^ 1][lane] = v;
         }
-        fsync<NT>();
-        if (lane < 12) sm.v0[lane] = at_apply(sm.v2, lane);
+        pb ^= 1;
         fsync<NT>();
       }
     }
-    if (lane < 12) sm.v0[lane] = 0.0;   // dx
+    if (lane < 16) sm.dx[0][lane] = 0.0;
     fsync<NT>();
+    int db = 0;
     for (int k = 0; k < N; ++k) {
-      if (lane < 12) sm.v1[lane] = sm.By[k][lane] - a_apply(sm.v0, lane);
-      fsync<NT>();
-      if (lane < 12) {
-        double w = 0.0;
+      double dxv[12], adx[12];
+      ld12(dxv, sm.dx[db]);
 #pragma unroll
-        for (int m = 0; m < 12; ++m) w = fma(sm.S[k][12 * lane + m], sm.v1[m], w);
-        sm.v2[lane] = w;
+      for (int i = 0; i < 12; ++i) {   // A dx on the 12-state
+        double a = dxv[i];
+        if (i < 3) a += sm.nmr[i][0] * dxv[6] + sm.nmr[i][1] * dxv[7] + sm.nmr[i][2] * dxv[8];
+        else if (i < 6) a += h * dxv[i + 6];
+        adx[i] = a;
+      }
+      if (lane < 12) {   // w = S_k (By - A dx)
+        double sr[12], by[12];
+        ld12(sr, sm.S[k] + 12 * lane);
+        ld12(by, sm.By[k]);
+#pragma unroll
+        for (int m = 0; m < 12; ++m) by[m] -= adx[m];
+        sm.w[lane] = dot12(sr, by);
       }
       fsync<NT>();
-      if (lane < NU) {
-        double z = 0.0;
-#pragma unroll
-        for (int i = 0; i < 12; ++i) z = fma(sm.Bm[i][lane], sm.v2[i], z);
-        sm.v1[lane] = z;
-      }
-      fsync<NT>();
-      if (lane < NU) {
+      if (lane < NU) {   // d = W B_leg^T w - Y
         const int l = lane / 3, a = lane % 3;
         const int j = sm.mt.stance_of[4 * k + l];
         double d = 0.0;
         if (j >= 0) {
-          const double* w = sm.W[j] + 3 * a;
-          d = w[0] * sm.v1[3 * l] + w[1] * sm.v1[3 * l + 1] + w[2] * sm.v1[3 * l + 2] - sm.Y[k][lane];
+          double w[12];
+          ld12(w, sm.w);
+          const double* wj = sm.W[j] + 3 * a;
+          d = wj[0] * dot12(bl0, w) + wj[1] * dot12(bl1, w) + wj[2] * dot12(bl2, w) - sm.Y[k][lane];
         }
         sm.dU[k][lane] = d;
       }
       fsync<NT>();
-      if (lane < 12) {
-        double v = a_apply(sm.v0, lane);
+      if (lane < 12) {   // dx <- A dx + B d
+        double du[12];
+        ld12(du, sm.dU[k]);
+        double a = adx[0];
 #pragma unroll
-        for (int c = 0; c < NU; ++c) v = fma(sm.Bm[lane][c], sm.dU[k][c], v);
-        sm.v2[lane] = v;
+        for (int i = 1; i < 12; ++i) a = (lane == i) ? adx[i] : a;
+        sm.dx[db ^ 1][lane] = a + dot12(brow, du);
       }
-      fsync<NT>();
-      if (lane < 12) sm.v0[lane] = sm.v2[lane];
+      db ^= 1;
       fsync<NT>();
     }
+    IPM_T1(2);
   };
 
-  // per-foot-step helpers
-  auto fvec = [&](const double (*A)[NU], int q, double (&o)[3]) {
-    const double* p = &A[jt[q]][3 * jl[q]];
-    o[0] = p[0];
-    o[1] = p[1];
-    o[2] = p[2];
-  };
-  auto adot = [&](int r, const double (&v)[3]) -> double {
-    return arow(r, 0) * v[0] + arow(r, 1) * v[1] + arow(r, 2) * v[2];
-  };
-  // W_j = (Rh_leg + sum_r d_r a_r a_r^T)^-1
-  auto set_w_ipm = [&](int q, const double (&d)[6]) {
-    double a[9];
-#pragma unroll
-    for (int x = 0; x < 3; ++x)
-#pragma unroll
-      for (int y = 0; y < 3; ++y) {
-        double v = (x == y) ? sm.rh[3 * jl[q] + x] : 0.0;
-#pragma unroll
-        for (int r = 0; r < 6; ++r)
-          if (live(r)) v = fma(d[r] * arow(r, x), arow(r, y), v);
-        a[3 * x + y] = v;
-      }
-    double o[9];
-    inv3(a, o);
-    double* w = sm.W[lane + LANES * q];
-#pragma unroll
-    for (int e = 0; e < 9; ++e) w[e] = o[e];
-  };
-
-  double s[IPM_FPL][6], lam[IPM_FPL][6];
   int status = MPCQP_STATUS_MAX_ITER;
   int nfact = 0;
 #ifdef MPCQP_IPM_DEBUG
@@ -446,127 +514,64 @@ __device__ void solve_robot_ipm(const KParams& KP, int b, IpmShared& sm, const f
     if (lane == 0 && Ug && dbg_n < N * NU) Ug[(size_t)b * N * NU + dbg_n] = (float)v;
     ++dbg_n;
   };
-  double dbg_p[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  double dbg_p[3] = {0.0, 0.0, 0.0};
 #endif
 
   // scales: gradient at U = 0 and the largest bound
   gradient();
   double gmax = 0.0, hmax = 0.0;
-#pragma unroll
-  for (int q = 0; q < IPM_FPL; ++q) {
-    if (!own[q]) continue;
+  for (int j = lane; j < S; j += NT) {
     double g[3];
-    fvec(sm.gr, q, g);
+    foot(j, sm.gr, g);
     gmax = fmax(gmax, fmax(fabs(g[0]), fmax(fabs(g[1]), fabs(g[2]))));
-    hmax = fmax(hmax, fabs(hb[q]));
+    hmax = fmax(hmax, sm.mt.ub[j]);
   }
-  const double gscale = 1.0 + sgpr_d(wave_max_all(gmax));
-  const double hscale = 1.0 + sgpr_d(wave_max_all(hmax));
+  const double gscale = 1.0 + sgpr_d(wave_max_d(gmax));
+  const double hscale = 1.0 + sgpr_d(wave_max_d(hmax));
   const double tol_g = 1e-9 * gscale, tol_h = 1e-9 * hscale;
 
   // ---- start: minimiser under a mild barrier weight, slacks shifted into the interior
-  {
+  for (int j = lane; j < S; j += NT) {
+    double d[6], rh[3], wv[9];
 #pragma unroll
-    for (int q = 0; q < IPM_FPL; ++q)
-      if (own[q]) {
-        double d[6];
+    for (int r = 0; r < 6; ++r) d[r] = 1e-2;
+    legrh(j, rh);
+    ipm_foot_weight(rw, liv, d, rh, wv);
 #pragma unroll
-        for (int r = 0; r < 6; ++r) d[r] = 1e-2;
-        set_w_ipm(q, d);
-      }
-    for (int e = lane; e < N * NU; e += NT) sm.rhs[e / NU][e % NU] = -sm.gr[e / NU][e % NU];
-    fsync<NT>();
-    factor();
-    ++nfact;
-    lsolve();
-    for (int e = lane; e < N * NU; e += NT) sm.U[e / NU][e % NU] = sm.dU[e / NU][e % NU];
-    fsync<NT>();
+    for (int e = 0; e < 9; ++e) sm.W[j][e] = wv[e];
+  }
+  for (int e = lane; e < N * NU; e += NT) sm.rhs[e / NU][e % NU] = -sm.gr[e / NU][e % NU];
+  fsync<NT>();
+  factor();
+  ++nfact;
+  lsolve();
+  for (int e = lane; e < N * NU; e += NT) sm.U[e / NU][e % NU] = sm.dU[e / NU][e % NU];
+  fsync<NT>();
+  for (int j = lane; j < S; j += NT) {
+    double f[3];
+    foot(j, sm.U, f);
+    const double h5 = -sm.mt.ub[j];
 #pragma unroll
-    for (int q = 0; q < IPM_FPL; ++q) {
-      double f[3];
-      fvec(sm.U, q, f);
-#pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        s[q][r] = own[q] && live(r) ? fmax(adot(r, f) - hrow(q, r), 1.0) : 1.0;
-        lam[q][r] = own[q] && live(r) ? 1.0 : 0.0;
-      }
+    for (int r = 0; r < 6; ++r) {
+      const bool on = (liv >> r) & 1;
+      sm.fs[j][r] = on ? fmax(adot(r, f) - (r == 5 ? h5 : 0.0), 1.0) : 1.0;
+      sm.fl[j][r] = on ? 1.0 : 0.0;
     }
   }
+  fsync<NT>();
 
-  // ---- active-set polish on the rows `act`; true when verified (sm.U = the optimum)
-  int act[IPM_FPL];
+  // ---- active-set polish on the rows sm.fact; true when verified (sm.U = the optimum)
   auto polish = [&]() -> bool {
-    double pj[IPM_FPL][9];
-    unsigned int nq_of[IPM_FPL];
+    for (int j = lane; j < S; j += NT) {
+      double rh[3], pj[9], fp[3], wv[9];
+      legrh(j, rh);
+      ipm_foot_nullspace(rw, sm.fact[j] & liv, -sm.mt.ub[j], rh, pj, fp, wv);
 #pragma unroll
-    for (int q = 0; q < IPM_FPL; ++q) {
-      pj[q][0] = 1.0; pj[q][1] = 0.0; pj[q][2] = 0.0;
-      pj[q][3] = 0.0; pj[q][4] = 1.0; pj[q][5] = 0.0;
-      pj[q][6] = 0.0; pj[q][7] = 0.0; pj[q][8] = 1.0;
-      nq_of[q] = 0;
-      if (!own[q]) continue;
-      // Gram-Schmidt of the active rows (row 5 first: the only one with h != 0)
-      double qv[3][3], L[3][3], fp[3] = {0.0, 0.0, 0.0}, c[3] = {0.0, 0.0, 0.0};
-      int nq = 0;
-      for (int o = 0; o < 6; ++o) {
-        const int r = o == 0 ? 5 : o - 1;
-        if (!((act[q] >> r) & 1) || !live(r) || nq == 3) continue;
-        double v[3] = {arow(r, 0), arow(r, 1), arow(r, 2)};
-        const double n0 = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
-        double coef[3] = {0.0, 0.0, 0.0};
-        for (int i = 0; i < nq; ++i) {
-          coef[i] = qv[i][0] * v[0] + qv[i][1] * v[1] + qv[i][2] * v[2];
-          v[0] -= coef[i] * qv[i][0];
-          v[1] -= coef[i] * qv[i][1];
-          v[2] -= coef[i] * qv[i][2];
-        }
-        const double nv = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
-        if (!(nv > 1e-9 * n0)) continue;   // dependent on the rows taken
-        for (int i = 0; i < nq; ++i) L[nq][i] = coef[i];
-        L[nq][nq] = nv;
-        qv[nq][0] = v[0] / nv;
-        qv[nq][1] = v[1] / nv;
-        qv[nq][2] = v[2] / nv;
-        // forward substitution of L c = h over the independent rows
-        double hv = hrow(q, r);
-        for (int i = 0; i < nq; ++i) hv -= L[nq][i] * c[i];
-        c[nq] = hv / nv;
-        ++nq;
+      for (int e = 0; e < 9; ++e) {
+        sm.W[j][e] = wv[e];
+        sm.fpj[j][e] = pj[e];
       }
-      for (int i = 0; i < nq; ++i)
-        for (int x = 0; x < 3; ++x) fp[x] += c[i] * qv[i][x];
-      for (int x = 0; x < 3; ++x)
-        for (int y = 0; y < 3; ++y) {
-          double v = (x == y) ? 1.0 : 0.0;
-          for (int i = 0; i < nq; ++i) v -= qv[i][x] * qv[i][y];
-          pj[q][3 * x + y] = v;
-        }
-      nq_of[q] = nq;
-      // W = P_j (P_j Rh P_j + I - P_j)^-1 P_j
-      double a[9], o[9];
-#pragma unroll
-      for (int x = 0; x < 3; ++x)
-#pragma unroll
-        for (int y = 0; y < 3; ++y) {
-          double v = -pj[q][3 * x + y] + ((x == y) ? 1.0 : 0.0);
-#pragma unroll
-          for (int z = 0; z < 3; ++z) v = fma(pj[q][3 * x + z] * sm.rh[3 * jl[q] + z], pj[q][3 * z + y], v);
-          a[3 * x + y] = v;
-        }
-      inv3(a, o);
-      double t[9];
-#pragma unroll
-      for (int x = 0; x < 3; ++x)
-#pragma unroll
-        for (int y = 0; y < 3; ++y)
-          t[3 * x + y] = o[3 * x] * pj[q][y] + o[3 * x + 1] * pj[q][3 + y] + o[3 * x + 2] * pj[q][6 + y];
-      double* w = sm.W[lane + LANES * q];
-#pragma unroll
-      for (int x = 0; x < 3; ++x)
-#pragma unroll
-        for (int y = 0; y < 3; ++y)
-          w[3 * x + y] = pj[q][3 * x] * t[y] + pj[q][3 * x + 1] * t[3 + y] + pj[q][3 * x + 2] * t[6 + y];
-      double* u = &sm.U[jt[q]][3 * jl[q]];
+      double* u = foot_ptr(j, sm.U);
       u[0] = fp[0];
       u[1] = fp[1];
       u[2] = fp[2];
@@ -578,86 +583,64 @@ __device__ void solve_robot_ipm(const KParams& KP, int b, IpmShared& sm, const f
       gradient();
       for (int e = lane; e < N * NU; e += NT) sm.rhs[e / NU][e % NU] = 0.0;
       fsync<NT>();
+      for (int j = lane; j < S; j += NT) {
+        double g[3];
+        foot(j, sm.gr, g);
+        const double* pj = sm.fpj[j];
+        double* r = foot_ptr(j, sm.rhs);
 #pragma unroll
-      for (int q = 0; q < IPM_FPL; ++q)
-        if (own[q]) {
-          double g[3];
-          fvec(sm.gr, q, g);
-          double* r = &sm.rhs[jt[q]][3 * jl[q]];
-#pragma unroll
-          for (int x = 0; x < 3; ++x) r[x] = -(pj[q][3 * x] * g[0] + pj[q][3 * x + 1] * g[1] + pj[q][3 * x + 2] * g[2]);
-        }
+        for (int x = 0; x < 3; ++x) r[x] = -(pj[3 * x] * g[0] + pj[3 * x + 1] * g[1] + pj[3 * x + 2] * g[2]);
+      }
       fsync<NT>();
       lsolve();
-#pragma unroll
-      for (int q = 0; q < IPM_FPL; ++q)
-        if (own[q]) {
-          double d[3];
-          fvec(sm.dU, q, d);
-          double* u = &sm.U[jt[q]][3 * jl[q]];
-          u[0] += d[0];
-          u[1] += d[1];
-          u[2] += d[2];
-        }
+      for (int j = lane; j < S; j += NT) {
+        double d[3];
+        foot(j, sm.dU, d);
+        double* u = foot_ptr(j, sm.U);
+        u[0] += d[0];
+        u[1] += d[1];
+        u[2] += d[2];
+      }
       fsync<NT>();
     }
     gradient();
     double stat = 0.0, smin = INFINITY, lminw = INFINITY;
-#ifdef MPCQP_IPM_DEBUG
-    double dbg_code = 0.0, dbg_r = 0.0;
-#endif
-#pragma unroll
-    for (int q = 0; q < IPM_FPL; ++q) {
-      if (!own[q]) continue;
+    for (int j = lane; j < S; j += NT) {
       double g[3], f[3];
-      fvec(sm.gr, q, g);
-      fvec(sm.U, q, f);
+      foot(j, sm.gr, g);
+      foot(j, sm.U, f);
+      const double* pj = sm.fpj[j];
 #pragma unroll
-      for (int x = 0; x < 3; ++x)
-        stat = fmax(stat, fabs(pj[q][3 * x] * g[0] + pj[q][3 * x + 1] * g[1] + pj[q][3 * x + 2] * g[2]));
+      for (int x = 0; x < 3; ++x) stat = fmax(stat, fabs(pj[3 * x] * g[0] + pj[3 * x + 1] * g[1] + pj[3 * x + 2] * g[2]));
       int viol = 0;
+      const double h5 = -sm.mt.ub[j];
 #pragma unroll
       for (int r = 0; r < 6; ++r)
-        if (live(r)) {
-          const double sl = adot(r, f) - hrow(q, r);
+        if ((liv >> r) & 1) {
+          const double sl = adot(r, f) - (r == 5 ? h5 : 0.0);
           smin = fmin(smin, sl);
           if (sl < -tol_h) viol |= 1 << r;
         }
-      // multipliers: g = sum lambda_r a_r over an independent subset of the active rows
-      const int am = act[q] & (implied ? 0x2F : 0x3F);
-      const int nq = (int)nq_of[q];
-      double best = nq == 0 ? INFINITY : -INFINITY;
+      const int am = sm.fact[j] & liv;
+      double best = INFINITY;
       int drop = -1;
-#ifdef MPCQP_IPM_DEBUG
-      double dbg_res = INFINITY;
-      int dbg_ndet = 0;
-#endif
-      if (nq > 0) {
-        double rw[6][3];
-#pragma unroll
-        for (int r = 0; r < 6; ++r)
-#pragma unroll
-          for (int x = 0; x < 3; ++x) rw[r][x] = arow(r, x);
+      if (am) {
+        double pjl[9], fpd[3], wd[9], rh[3];
+        legrh(j, rh);
+        const int nq = ipm_foot_nullspace(rw, am, h5, rh, pjl, fpd, wd);
         ipm_cone_multipliers(rw, am, nq, g, tol_g, best, drop);
       }
-#ifdef MPCQP_IPM_DEBUG
-      if (best == -INFINITY && dbg_code == 0.0) {
-        dbg_code = am * 1000 + nq * 100 + dbg_ndet + 0.5;
-        dbg_r = fmax(fabs(g[0]), fmax(fabs(g[1]), fabs(g[2])));
-      }
-#endif
       lminw = fmin(lminw, best);
-      act[q] = (act[q] | viol) & ~(drop >= 0 ? (1 << drop) : 0);
+      sm.fact[j] = (sm.fact[j] | viol) & ~(drop >= 0 ? (1 << drop) : 0);
     }
-    stat = wave_max_all(stat);
-    smin = wave_min_all(smin);
-    lminw = wave_min_all(lminw);
+    stat = wave_max_d(stat);
+    smin = wave_min(smin);
+    lminw = wave_min(lminw);
+    fsync<NT>();
 #ifdef MPCQP_IPM_DEBUG
     dbg_p[0] = stat / gscale;
     dbg_p[1] = smin;
     dbg_p[2] = lminw;
-    dbg_p[3] = wave_max_all(dbg_code);
-    dbg_p[4] = wave_max_all(dbg_code > 0.0 ? dbg_r : 0.0);
 #endif
     return stat < IPM_STAT_TOL * gscale && smin > -tol_h && lminw > -tol_g;
   };
@@ -668,185 +651,167 @@ __device__ void solve_robot_ipm(const KParams& KP, int b, IpmShared& sm, const f
   while (!done && it < IPM_MAX_IT) {
     ++it;
     gradient();
-    double rd[IPM_FPL][3], rp[IPM_FPL][6];
+    // residuals rd = g - G^T lam, rp = G f - h - s; mu
     double sl = 0.0;
-#pragma unroll
-    for (int q = 0; q < IPM_FPL; ++q) {
+    for (int j = lane; j < S; j += NT) {
       double g[3], f[3];
-      fvec(sm.gr, q, g);
-      fvec(sm.U, q, f);
+      foot(j, sm.gr, g);
+      foot(j, sm.U, f);
+      const double h5 = -sm.mt.ub[j];
 #pragma unroll
       for (int x = 0; x < 3; ++x) {
         double v = g[x];
 #pragma unroll
-        for (int r = 0; r < 6; ++r) v = fma(-lam[q][r], arow(r, x), v);
-        rd[q][x] = own[q] ? v : 0.0;
+        for (int r = 0; r < 6; ++r) v = fma(-sm.fl[j][r], rw[r][x], v);
+        sm.frd[j][x] = v;
       }
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
-        const bool on = own[q] && live(r);
-        rp[q][r] = on ? adot(r, f) - hrow(q, r) - s[q][r] : 0.0;
-        sl += on ? s[q][r] * lam[q][r] : 0.0;
+        const bool on = (liv >> r) & 1;
+        sm.frp[j][r] = on ? adot(r, f) - (r == 5 ? h5 : 0.0) - sm.fs[j][r] : 0.0;
+        sl += on ? sm.fs[j][r] * sm.fl[j][r] : 0.0;
       }
     }
     const double mu = sgpr_d(wave_sum_d(sl)) / m_tot;
 #ifdef MPCQP_IPM_DEBUG
-    {
-      double rdm = 0.0, rpm = 0.0;
-#pragma unroll
-      for (int q = 0; q < IPM_FPL; ++q) {
-#pragma unroll
-        for (int x = 0; x < 3; ++x) rdm = fmax(rdm, fabs(rd[q][x]));
-#pragma unroll
-        for (int r = 0; r < 6; ++r) rpm = fmax(rpm, fabs(rp[q][r]));
-      }
-      rdm = wave_max_all(rdm);
-      rpm = wave_max_all(rpm);
-      dbg((double)it);
-      dbg(mu);
-      dbg(rdm);
-      dbg(rpm);
-      dbg(dbg_p[0]);
-      dbg(dbg_p[1]);
-      dbg(dbg_p[2]);
-      dbg(dbg_p[3]);
-      dbg(dbg_p[4]);
-    }
+    dbg((double)it);
+    dbg(mu);
+    dbg(dbg_p[0]);
+    dbg(dbg_p[1]);
+    dbg(dbg_p[2]);
+    dbg((double)nfact);
+    dbg(gscale);
+    dbg(hscale);
 #endif
     if (mu < IPM_POLISH_MU * gscale * hscale) {
-#pragma unroll
-      for (int q = 0; q < IPM_FPL; ++q) {
-        act[q] = 0;
+      for (int j = lane; j < S; j += NT) {
+        int a = 0;
 #pragma unroll
         for (int r = 0; r < 6; ++r)
-          if (own[q] && live(r) && lam[q][r] > s[q][r]) act[q] |= 1 << r;
+          if (((liv >> r) & 1) && sm.fl[j][r] > sm.fs[j][r]) a |= 1 << r;
+        sm.fact[j] = a;
       }
       // U is overwritten by the polish: keep the IPM iterate
       for (int e = lane; e < N * NU; e += NT) sm.Us[e / NU][e % NU] = sm.U[e / NU][e % NU];
       fsync<NT>();
       for (int corr = 0; corr <= IPM_NCORR; ++corr) {
-        int before[IPM_FPL];
-#pragma unroll
-        for (int q = 0; q < IPM_FPL; ++q) before[q] = act[q];
+        int changed = 0;
+        for (int j = lane; j < S; j += NT) sm.fprev[j] = sm.fact[j];
+        fsync<NT>();
         if (polish()) {
           done = true;
           status = MPCQP_STATUS_OK;
           break;
         }
-        int same = 1;
-#pragma unroll
-        for (int q = 0; q < IPM_FPL; ++q) same &= before[q] == act[q];
-        if (__all(same)) break;
+        for (int j = lane; j < S; j += NT) changed |= sm.fact[j] != sm.fprev[j];
+        if (!__any(changed)) break;
       }
       if (done) break;
       for (int e = lane; e < N * NU; e += NT) sm.U[e / NU][e % NU] = sm.Us[e / NU][e % NU];
       fsync<NT>();
     }
-    double D[IPM_FPL][6];
+    for (int j = lane; j < S; j += NT) {
+      double d[6], rh[3], wv[9];
 #pragma unroll
-    for (int q = 0; q < IPM_FPL; ++q) {
+      for (int r = 0; r < 6; ++r) d[r] = ((liv >> r) & 1) ? sm.fl[j][r] / sm.fs[j][r] : 0.0;
+      legrh(j, rh);
+      ipm_foot_weight(rw, liv, d, rh, wv);
 #pragma unroll
-      for (int r = 0; r < 6; ++r) D[q][r] = own[q] && live(r) ? lam[q][r] / s[q][r] : 0.0;
-      if (own[q]) set_w_ipm(q, D[q]);
+      for (int e = 0; e < 9; ++e) sm.W[j][e] = wv[e];
     }
     fsync<NT>();
     factor();
     ++nfact;
-    // Newton direction for the complementarity target rc (per row); ds, dl out
-    double ds[IPM_FPL][6], dl[IPM_FPL][6];
-    auto newton = [&](const double (&rc)[IPM_FPL][6]) {
+    // Newton direction for the complementarity target: predictor (sig = 0, corr = false)
+    // or corrector (target mu, the affine ds dl second-order term)
+    auto newton = [&](bool corr, double target) {
       for (int e = lane; e < N * NU; e += NT) sm.rhs[e / NU][e % NU] = 0.0;
       fsync<NT>();
+      for (int j = lane; j < S; j += NT) {
+        double* rr = foot_ptr(j, sm.rhs);
 #pragma unroll
-      for (int q = 0; q < IPM_FPL; ++q)
-        if (own[q]) {
-          double* rr = &sm.rhs[jt[q]][3 * jl[q]];
+        for (int x = 0; x < 3; ++x) {
+          double v = -sm.frd[j][x];
 #pragma unroll
-          for (int x = 0; x < 3; ++x) {
-            double v = -rd[q][x];
-#pragma unroll
-            for (int r = 0; r < 6; ++r)
-              if (live(r)) v = fma(arow(r, x), rc[q][r] / s[q][r] - D[q][r] * rp[q][r], v);
-            rr[x] = v;
-          }
-        }
-      fsync<NT>();
-      lsolve();
-#pragma unroll
-      for (int q = 0; q < IPM_FPL; ++q) {
-        double d[3];
-        fvec(sm.dU, q, d);
-#pragma unroll
-        for (int r = 0; r < 6; ++r) {
-          const bool on = own[q] && live(r);
-          ds[q][r] = on ? adot(r, d) + rp[q][r] : 0.0;
-          dl[q][r] = on ? (rc[q][r] - lam[q][r] * ds[q][r]) / s[q][r] : 0.0;
+          for (int r = 0; r < 6; ++r)
+            if ((liv >> r) & 1) {
+              const double s_ = sm.fs[j][r], l_ = sm.fl[j][r];
+              const double rc = -s_ * l_ + (corr ? target - sm.fds[j][r] * sm.fdl[j][r] : 0.0);
+              v = fma(rw[r][x], rc / s_ - (l_ / s_) * sm.frp[j][r], v);
+            }
+          rr[x] = v;
         }
       }
-    };
-    auto max_steps = [&](double& ap, double& ad) {
+      fsync<NT>();
+      lsolve();
       double a1 = 1.0, a2 = 1.0;
+      for (int j = lane; j < S; j += NT) {
+        double d[3];
+        foot(j, sm.dU, d);
 #pragma unroll
-      for (int q = 0; q < IPM_FPL; ++q)
-#pragma unroll
-        for (int r = 0; r < 6; ++r) {
-          if (ds[q][r] < 0.0) a1 = fmin(a1, -s[q][r] / ds[q][r]);
-          if (dl[q][r] < 0.0) a2 = fmin(a2, -lam[q][r] / dl[q][r]);
-        }
-      ap = sgpr_d(wave_min_all(a1));
-      ad = sgpr_d(wave_min_all(a2));
+        for (int r = 0; r < 6; ++r)
+          if ((liv >> r) & 1) {
+            const double s_ = sm.fs[j][r], l_ = sm.fl[j][r];
+            const double rc = -s_ * l_ + (corr ? target - sm.fds[j][r] * sm.fdl[j][r] : 0.0);
+            const double ds = adot(r, d) + sm.frp[j][r];
+            const double dl = (rc - l_ * ds) / s_;
+            sm.fds[j][r] = ds;
+            sm.fdl[j][r] = dl;
+            if (ds < 0.0) a1 = fmin(a1, -s_ / ds);
+            if (dl < 0.0) a2 = fmin(a2, -l_ / dl);
+          }
+      }
+      return d2{sgpr_d(wave_min(a1)), sgpr_d(wave_min(a2))};
     };
-    double rc[IPM_FPL][6];
-#pragma unroll
-    for (int q = 0; q < IPM_FPL; ++q)
-#pragma unroll
-      for (int r = 0; r < 6; ++r) rc[q][r] = -s[q][r] * lam[q][r];
-    newton(rc);
-    double ap, ad;
-    max_steps(ap, ad);
+    d2 al = newton(false, 0.0);
     double sa = 0.0;
-#pragma unroll
-    for (int q = 0; q < IPM_FPL; ++q)
+    for (int j = lane; j < S; j += NT)
 #pragma unroll
       for (int r = 0; r < 6; ++r)
-        if (own[q] && live(r)) sa += (s[q][r] + ap * ds[q][r]) * (lam[q][r] + ad * dl[q][r]);
+        if ((liv >> r) & 1) sa += (sm.fs[j][r] + al[0] * sm.fds[j][r]) * (sm.fl[j][r] + al[1] * sm.fdl[j][r]);
     const double mu_aff = sgpr_d(wave_sum_d(sa)) / m_tot;
     const double sig = mu_aff / mu;
     const double target = fmax(sig * sig * sig * mu, IPM_MU_FLOOR * gscale * hscale);
-#pragma unroll
-    for (int q = 0; q < IPM_FPL; ++q)
-#pragma unroll
-      for (int r = 0; r < 6; ++r) rc[q][r] = -s[q][r] * lam[q][r] - ds[q][r] * dl[q][r] + target;
-    newton(rc);
-    max_steps(ap, ad);
-    ap = fmin(1.0, IPM_TAU * ap);
-    ad = fmin(1.0, IPM_TAU * ad);
-#pragma unroll
-    for (int q = 0; q < IPM_FPL; ++q) {
-      if (own[q]) {
-        double d[3];
-        fvec(sm.dU, q, d);
-        double* u = &sm.U[jt[q]][3 * jl[q]];
-        u[0] += ap * d[0];
-        u[1] += ap * d[1];
-        u[2] += ap * d[2];
-      }
+    fsync<NT>();
+    al = newton(true, target);
+    const double ap = fmin(1.0, IPM_TAU * al[0]), ad = fmin(1.0, IPM_TAU * al[1]);
+    for (int j = lane; j < S; j += NT) {
+      double d[3];
+      foot(j, sm.dU, d);
+      double* u = foot_ptr(j, sm.U);
+      u[0] += ap * d[0];
+      u[1] += ap * d[1];
+      u[2] += ap * d[2];
 #pragma unroll
       for (int r = 0; r < 6; ++r)
-        if (own[q] && live(r)) {
-          s[q][r] += ap * ds[q][r];
-          lam[q][r] += ad * dl[q][r];
+        if ((liv >> r) & 1) {
+          sm.fs[j][r] += ap * sm.fds[j][r];
+          sm.fl[j][r] += ad * sm.fdl[j][r];
         }
     }
     fsync<NT>();
   }
 
-  // ------------------------------------------------ output (U: the polished optimum or the last iterate)
+  // ------------------------------------------------ output (the polished optimum or the last iterate)
   bool finite = true;
   for (int e = lane; e < N * NU; e += NT) finite &= isfinite(sm.U[e / NU][e % NU]);
   if (__any(!finite)) status = MPCQP_STATUS_NONFINITE;
   if (lane < 12) u0g[(size_t)b * 12 + lane] = (float)sm.U[0][lane];
 #ifdef MPCQP_IPM_DEBUG
+  {   // the last 8 slots: cycles in gradient / factor / lsolve / total, factor T / GJ / S store / sym
+    const unsigned long long tot = __builtin_amdgcn_s_memtime() - cyc_t0;
+    if (lane == 0 && Ug) {
+      float* dst = Ug + (size_t)b * N * NU + N * NU - 8;
+      dst[0] = (float)cyc[0];
+      dst[1] = (float)cyc[1];
+      dst[2] = (float)cyc[2];
+      dst[3] = (float)tot;
+      dst[4] = (float)cyc[4];
+      dst[5] = (float)cyc[5];
+      dst[6] = (float)cyc[6];
+      dst[7] = (float)cyc[7];
+    }
+  }
   Ug = nullptr;
 #endif
   if (Ug)

@@ -49,8 +49,11 @@ torch.cuda.synchronize()
 assert rc == 0, rc
 D = Ud.cpu().numpy()
 for i, c in enumerate(cases):
-    print(f"--- case {c} trace (it, mu, rd, rp, stat/g, slack min, lam min, code am*1000+nq*100+ndet, min res)")
-    tr = D[i][:N * 12 // 9 * 9].reshape(-1, 9)
+    print(f"--- case {c} trace (it, mu, polish stat/g, slack min, lam min, nfact, gscale, hscale)")
+    cyc = D[i][N * 12 - 8:]
+    print(f"    cycles: gradient {cyc[0]:.3g} factor {cyc[1]:.3g} lsolve {cyc[2]:.3g} total {cyc[3]:.3g}; "
+          f"factor T {cyc[4]:.3g} GJ {cyc[5]:.3g} S store {cyc[6]:.3g} sym {cyc[7]:.3g}")
+    tr = D[i][:(N * 12 - 8) // 8 * 8].reshape(-1, 8)
     for row in tr:
         if row[0] == 0:
             break
