@@ -60,34 +60,25 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(bt, N, budget_s, rows=None):
-    """Reference-faithful NumPy formulation + exact float64 QP solve, 1 core
-    (robots `rows` of the batch, default all)."""
-    try:
-        from threadpoolctl import threadpool_limits
-        lim = threadpool_limits(1)
-    except Exception:
-        lim = None
-    from oracle import formulation as F
-    from oracle import qp as Q
-    import numpy as np
+def cpu_baseline(bt, N, budget_s, threads=1):
+    """The compiled CPU restatement of the reference's per-tick formulate + solve
+    (oracle/cpu_mpc.cpp: float32 model and dense condensing as mpc.py:173-233 builds them,
+    float64 Goldfarb-Idnani solve), OpenMP over the batch's robots with `threads`
+    threads, cycling over the batch until `budget_s` is spent.  Returns robots / s, robots
+    solved, wall seconds, and the formulation / solve thread-seconds per robot."""
+    from oracle import cpu_port
+    cpu_port.solve_batch({k: v[:8] for k, v in bt.items()}, N, threads=threads)   # warm the pool
     t0 = time.perf_counter()
-    done = 0
-    for b in (range(bt["x0"].shape[0]) if rows is None else rows):
-        rec = bt["robot"][b]
-        inertia = np.array([[rec[1], rec[2], rec[3]], [rec[2], rec[4], rec[5]],
-                            [rec[3], rec[5], rec[6]]], dtype=np.float32)
-        o = F.formulate(bt["x0"][b], bt["xref"][b].reshape(-1), bt["contact"][b].reshape(-1),
-                        bt["feet"][b].astype(np.float64), inertia, float(rec[0]), N,
-                        mu=float(rec[7]), fz_max=float(rec[8]))
-        Q.solve_qp_dual_active_set(o["H"], o["g"], o["C"], o["lb"], o["ub"])
-        done += 1
-        if time.perf_counter() - t0 > budget_s and done >= 3:
+    done, tf, ts = 0, 0.0, 0.0
+    while True:
+        _, _, f, s_ = cpu_port.solve_batch(bt, N, threads=threads)
+        done += int(bt["x0"].shape[0])
+        tf += f
+        ts += s_
+        if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
-    if lim is not None:
-        lim.unregister() if hasattr(lim, "unregister") else None
-    return done / dt, done, dt
+    return done / dt, done, dt, tf / done, ts / done
 
 
 def _cpu_model():
@@ -101,39 +92,13 @@ def _cpu_model():
     return "unknown CPU"
 
 
-def _cpu_worker(job):
-    bt, N, budget_s, rows = job
-    return cpu_baseline(bt, N, budget_s, rows)
-
-
-def cpu_baseline_all_cores(bt, N, budget_s):
-    """The same CPU port on every host core this job may use (one process per core,
-    robots dealt round-robin).  Rate = robots solved / slowest worker's
-    solve time (process start-up excluded)."""
-    import multiprocessing as mp
+def _host_cores():
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
-    procs = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", "16")), 16))
-    B = bt["x0"].shape[0]
-    env_keep = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")}
-    for k in env_keep:
-        os.environ[k] = "1"
-    try:
-        with mp.get_context("spawn").Pool(procs) as pool:
-            # each worker cycles over its robots until its time budget is spent
-            res = pool.map(_cpu_worker, [(bt, N, budget_s, list(range(w, B, procs)) * 1000)
-                                         for w in range(procs)])
-    finally:
-        for k, v in env_keep.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-    done = sum(r[1] for r in res)
-    dt = max(r[2] for r in res)
-    return done / dt, done, dt, procs
+    # the box's share: OMP_NUM_THREADS / MAX_JOBS are set to it (16 for one GPU)
+    return max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", "16")), 16))
 
 
 def time_callers(eng, h, B, N, dev, stream, reps=20):
@@ -288,7 +253,6 @@ def bench_config1(args):
     sys.path.insert(0, os.path.join(ROOT, "pympc-quadruped_amd", "linear_mpc"))
     import importlib
     mpc = importlib.import_module("mpc")
-    from mpcqp.params import ROBOT_PRESETS
     from mpcqp.synthetic import gait_table
     from oracle import formulation as F
 
@@ -333,17 +297,18 @@ def bench_config1(args):
     assert np.all(np.isfinite(u))
     cpu = None
     if not args.no_cpu:
-        from oracle import qp as Q
-        t0 = time.perf_counter()
-        done = 0
-        while time.perf_counter() - t0 < args.cpu_seconds and done < 10 * len(states):
-            x0, xr, tb, feet = states[done % len(states)]
-            o = F.formulate(x0, xr, tb, feet, al["inertia"], al["mass"], N)
-            Q.solve_qp_dual_active_set(o["H"], o["g"], o["C"], o["lb"], o["ub"])
-            done += 1
-        cpu = {"value": (time.perf_counter() - t0) / done * 1e3, "unit": "ms/tick", "cores": 1, "kind": "port",
-               "sample": f"{done} MPC ticks of the same run's states ({_cpu_model()}): reference-faithful NumPy "
-                         "formulation (oracle/formulation.py) + exact float64 dual active set (oracle/qp.py)"}
+        from mpcqp.params import pack_robot, ROBOT_PRESETS
+        rec = pack_robot(ROBOT_PRESETS["aliengo"])
+        bt = {"x0": np.stack([st[0] for st in states]), "xref": np.stack([st[1] for st in states]),
+              "contact": np.stack([st[2] for st in states]),
+              "feet": np.stack([np.asarray(st[3], np.float32).reshape(12) for st in states]),
+              "robot": np.tile(rec, (len(states), 1))}
+        rate, done, dt, f1, s1 = cpu_baseline(bt, N, args.cpu_seconds, threads=1)
+        cpu = {"value": dt / done * 1e3, "unit": "ms/tick", "cores": 1, "kind": "port",
+               "formulation_ms": f1 * 1e3, "solve_ms": s1 * 1e3,
+               "sample": f"{done} MPC ticks of the same run's states, 1 thread ({_cpu_model()}): compiled "
+                         "restatement of the reference's formulation + float64 Goldfarb-Idnani QP "
+                         "(oracle/cpu_mpc.cpp)"}
     med = float(np.median(mpc_ms))
     print(json.dumps({
         "metric": "drop-in MPC tick latency (B=1, Aliengo, horizon 16, trot10)",
@@ -513,15 +478,17 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu:
-            v1, done1, dt1 = cpu_baseline(host[0], N, args.cpu_seconds)
-            vm, donem, dtm, procs = cpu_baseline_all_cores(host[0], N, args.cpu_seconds / 2)
+            procs = _host_cores()
+            v1, done1, dt1, f1, s1 = cpu_baseline(host[0], N, args.cpu_seconds / 2, threads=1)
+            vm, donem, dtm, fm, sm_ = cpu_baseline(host[0], N, args.cpu_seconds / 2, threads=procs)
             cpu = {"value": vm, "unit": "QP/s", "cores": procs, "kind": "port",
-                   "sample": f"{donem} robot solves (the config's first synthetic batch, cycled) in {dtm:.1f}s on "
-                             f"{procs} processes x 1 thread ({_cpu_model()}): reference-faithful NumPy "
-                             "formulation (oracle/formulation.py) + exact float64 dual active-set QP "
-                             "(oracle/qp.py)",
-                   "single_core": {"value": v1, "cores": 1,
-                                   "sample": f"{done1} robots in {dt1:.1f}s, 1 process x 1 thread"}}
+                   "sample": f"{donem} robot solves (the config's first synthetic batch, cycled) in {dtm:.1f}s, "
+                             f"OpenMP {procs} threads ({_cpu_model()}): compiled restatement of the reference's "
+                             "formulation (float32 model, dense condensing, mpc.py:173-260) + float64 "
+                             "Goldfarb-Idnani QP (oracle/cpu_mpc.cpp, g++ -O3)",
+                   "formulation_us_per_robot": fm * 1e6, "solve_us_per_robot": sm_ * 1e6,
+                   "single_core": {"value": v1, "cores": 1, "formulation_us": f1 * 1e6, "solve_us": s1 * 1e6,
+                                   "sample": f"{done1} robots in {dt1:.1f}s, 1 thread"}}
         line = {
             "metric": "QP solves/sec (whole node), horizon=10 GRF QP, at 1/2/4/8 MI355X",
             "value": qps,

@@ -58,7 +58,11 @@ extern "C" {
 #define MPCQP_ERR_ALLOC -3
 
 /* per-robot status */
-#define MPCQP_STATUS_OK 0          /* KKT verified */
+#define MPCQP_STATUS_OK 0          /* the optimum: every cone row feasible, every active
+                                      multiplier >= 0 (checked); stationarity holds by
+                                      construction of the dual active-set updates (dense
+                                      classes) or is checked on the active set's null
+                                      space (interior-point class, n > 128) */
 #define MPCQP_STATUS_MAX_ITER 1    /* iteration cap hit: best iterate returned */
 #define MPCQP_STATUS_INFEASIBLE 2  /* cannot happen for this QP (U = 0 is feasible) */
 #define MPCQP_STATUS_TOO_LARGE 3   /* stance variables exceed the engine's capacity */

@@ -282,6 +282,17 @@ __device__ __forceinline__ int wave_argmin_f32(double v, double& vmin_out) {
 #include "mpcqp_ipm.h"
 #include "mpcqp_plan.h"
 
+// Workgroups are dealt round-robin over the 8 XCDs (block bid runs on XCD bid % 8,
+// MI355X_MICROARCH.md "Workgroup dispatch"; speed only, never correctness).  Block bid
+// solves robot xcd_robot(bid, B): each XCD takes one contiguous range of robots, so
+// neighbouring robots -- whose input records and u0 / status / iters entries share
+// cache lines -- meet in one L2 and their lines are fetched and written back once.
+// A bijection of [0, B) for every B.
+__device__ __forceinline__ int xcd_robot(int bid, int B) {
+  const int x = bid & 7, i = bid >> 3, q = B >> 3, r = B & 7;
+  return x * q + (x < r ? x : r) + i;
+}
+
 // Class NV = 64: one 2-wave workgroup per robot of the batch.  Robots with more
 // than 64 stance variables are appended to `queue` (when given) for class 96, those
 // with more than 96 to `queue_big` (when given) for class 128.
@@ -291,8 +302,8 @@ __global__ __launch_bounds__(Cfg<64>::NT) __attribute__((amdgpu_waves_per_eu(2, 
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
     int* __restrict__ queue, int* __restrict__ queue_big, int* __restrict__ queue_ipm) {
   __shared__ SharedT<64> sm;
-  const int b = blockIdx.x;
-  if (b >= B) return;
+  if ((int)blockIdx.x >= B) return;
+  const int b = xcd_robot(blockIdx.x, B);
   solve_robot<64>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, queue, queue_big,
                   queue_ipm);
 }
