@@ -187,7 +187,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   const int N = P.N;
 #ifdef MPCQP_STAMPS
   unsigned long long stamps_[7];
-  unsigned long long secacc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, seclast_ = 0;
+  unsigned long long secacc_[16] = {}, seclast_ = 0;
   int seccur_ = 7;
 #endif
   STAMP(0);
@@ -465,6 +465,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       c0 = (int)((unsigned)v0 % TW);
       sp = sgpr_d(vmn);   // s_p, tracked like s[] (identical arithmetic)
       up = 0.0;
+      SEC(8);
       // second candidate: the best row of any other foot-step
       if constexpr (SharedT<NV>::kPair) {
       double bw = INFINITY;
@@ -541,6 +542,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     double* const vr2 = sm.vr2[buf];
     combo_store(c0, tcA, a0, a1, a2, vz, vr);
     if (p2 >= 0) combo_store(c02, tcA2, b0, b1, b2, vz2, vr2);
+    SEC(9);
     fsync<NT>();
     SEC(2);
     // constraint-row steps zs = A z, slot directions r, variable steps
@@ -551,6 +553,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
     for (int k = 1; k < CPL; ++k) zsp = (k == (p >> 6)) ? zs[k] : zsp;
     zsp = readlane_d(zsp, p & 63);   // lane p computed a_p . z exactly as zs
+    SEC(10);
 
     // ---- pair step: add p and p2 together when the equality-constrained solution
     // on A + {p, p2} keeps every multiplier positive.  With Z = [z, z2] and the 2x2
@@ -658,6 +661,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         continue;
       }
     }
+    SEC(11);
     double rs[VPL], zx[VPL];
     double rbest = INFINITY;
     int lk = 0;
@@ -674,6 +678,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     double t1;
     const int ll = wave_argmin_d(rbest, t1);
     const int l = ll + LANES * uni(__builtin_amdgcn_readlane(lk, ll));
+    SEC(12);
     double t2 = INFINITY;
     if (zsp > thr) t2 = div_nr(-sp, zsp);
     const bool add = t2 <= t1;
@@ -765,6 +770,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       for (int k = 0; k < VPL; ++k) u[k] = (lane + LANES * k == l) ? 0.0 : u[k];
       occ[l >> 6] &= ~(1ull << (l & 63));
     }
+    SEC(13);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -821,7 +827,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   if (tid == 0 && Ug) {
     unsigned long long* dst = (unsigned long long*)(Ug + (size_t)b * N * 12);
     for (int i = 0; i < 7; ++i) dst[i] = stamps_[i];
-    for (int i = 0; i < 8; ++i) dst[8 + i] = secacc_[i];
+    for (int i = 0; i < 16; ++i) dst[8 + i] = secacc_[i];
   }
   Ug = nullptr;
 #endif

@@ -56,8 +56,9 @@ def main():
     sel = iters > 0
     print(f"  active-set cycles / iteration: median {np.median(gi[sel] / iters[sel]):.0f}")
     sec = U.cpu().numpy().reshape(B, -1).view(np.uint64)[:, 8:24].astype(np.int64)
-    names = ["loop top + argmin p", "colcombo", "zs/r gathers", "-", "-", "add: q, 1/s, loads, coefs", "drop path", "-",
-             "a_p setup", "store + barrier", "ratio argmin", "t2, step", "rank-1 FMAs", "-", "-", "-"]
+    names = ["argmin p + a_p rows", "barrier", "zs = A z (LDS)", "-", "-", "add: q, 1/s, loads, coefs",
+             "drop: R_l, H R_l, R H R_l", "-", "pair candidate", "combo + LDS store", "pair-step test",
+             "ratio test (loads, div, argmin)", "t2, step, x/u/s", "rank-1 FMAs (P, R)", "-", "-"]
     tot_it = iters[sel].sum()
     for k, name in enumerate(names):
         if name != "-":
