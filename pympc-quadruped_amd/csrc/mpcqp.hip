@@ -40,6 +40,12 @@ constexpr int NX = 13;      // state dimension (mpc.py:26)
 constexpr int NU = 12;      // input dimension (mpc.py:28)
 constexpr int LANES = 64;
 constexpr int kMaxN = 20;   // LDS scratch is sized for N <= 20
+#ifndef MPCQP_C64_TW
+#define MPCQP_C64_TW 8   // class-64 register tile width (8: 2 waves per robot; 4: 4 waves, slower)
+#endif
+#ifndef MPCQP_C64_WPE
+#define MPCQP_C64_WPE (MPCQP_C64_TW == 4 ? 4 : 2)   // class-64 waves per SIMD (VGPR budget)
+#endif
 // staged inputs (floats)
 constexpr int IN_X0 = 0, IN_FEET = 13, IN_ROBOT = 25, IN_CONTACT = 44, IN_XREF = 44 + 4 * kMaxN;
 constexpr int IN_END = IN_XREF + NX * kMaxN;
@@ -64,16 +70,23 @@ struct KParams {
     stamps_[i] = __builtin_amdgcn_s_memtime();  \
     __builtin_amdgcn_sched_barrier(0);          \
   } while (0)
+// section accumulators live one per lane (lane k holds section k): a uniform
+// compare, no runtime-indexed private array (that would go to scratch, and the
+// next barrier's vmcnt wait would absorb the scratch latency)
 #define SEC(k)                                                   \
   do {                                                           \
     __builtin_amdgcn_sched_barrier(0);                           \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime();  \
-    secacc_[seccur_] += t_ - seclast_;                           \
+    if (lane == seccur_) secacc_ += t_ - seclast_;               \
     seclast_ = t_;                                               \
     seccur_ = (k);                                               \
     __builtin_amdgcn_sched_barrier(0);                           \
   } while (0)
+#define CNT(k) (secacc_ += (lane == (k)) ? 1ull : 0ull)
 #else
+#define CNT(k) \
+  do {         \
+  } while (0)
 #define STAMP(i) \
   do {           \
   } while (0)
@@ -296,7 +309,7 @@ __device__ __forceinline__ int xcd_robot(int bid, int B) {
 // Class NV = 64: one 2-wave workgroup per robot of the batch.  Robots with more
 // than 64 stance variables are appended to `queue` (when given) for class 96, those
 // with more than 96 to `queue_big` (when given) for class 128.
-__global__ __launch_bounds__(Cfg<64>::NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void mpcqp_kernel_64(
+__global__ __launch_bounds__(Cfg<64>::NT) __attribute__((amdgpu_waves_per_eu(MPCQP_C64_WPE, Cfg<64>::NW))) void mpcqp_kernel_64(
     KParams P, int B, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,

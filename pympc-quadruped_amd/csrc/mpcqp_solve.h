@@ -27,7 +27,8 @@
 
 template <int NV>
 struct Cfg {
-  static constexpr int TW = NV == 96 ? 6 : 8;   // tile width: 4 x TW register tiles
+  // tile width: 4 x TW register tiles (class 64: TW = 4 spreads a robot over 4 waves)
+  static constexpr int TW = NV == 96 ? 6 : (NV == 64 ? MPCQP_C64_TW : 8);
   static constexpr int NW = NV * NV / (4 * TW * LANES);   // waves per robot
   static constexpr int NT = NW * LANES;
   static constexpr int TCN = NV / TW;         // tile columns (lanes per tile row)
@@ -187,7 +188,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   const int N = P.N;
 #ifdef MPCQP_STAMPS
   unsigned long long stamps_[7];
-  unsigned long long secacc_[16] = {}, seclast_ = 0;
+  unsigned long long secacc_ = 0, seclast_ = 0;
   int seccur_ = 7;
 #endif
   STAMP(0);
@@ -455,6 +456,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       for (int k = 1; k < CPL; ++k) sv = (k == kp) ? s[k] : sv;
       const double vmn = readlane_d(sv, pl);
       p = pl + LANES * kp;
+      CNT(4);
       const int rp = p % 6;
       a0 = sgpr_d(sm.mt.rows[rp][0]);
       a1 = sgpr_d(sm.mt.rows[rp][1]);
@@ -511,6 +513,13 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       if constexpr (TW == 6) {   // foot-steps start at register column 0 or 3: never straddle
         if (cA == 0) colcombo<0, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq);
         else colcombo<3, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq);
+      } else if constexpr (TW == 4) {
+        switch (cA) {
+          case 0: colcombo<0, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+          case 1: colcombo<1, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+          case 2: colcombo<2, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+          default: colcombo<3, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+        }
       } else {
         switch (cA) {
           case 0: colcombo<0, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
@@ -523,7 +532,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
           default: colcombo<7, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
         }
       }
-      if (TW == 8 && cA >= 6) {   // the foot-step straddles tile columns tA, tA + 1 (next lane)
+      if (TW != 6 && cA + 2 >= TW) {   // the foot-step straddles tile columns tA, tA + 1 (next lane)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           zq[r] += dpp_shl1(zq[r]);
@@ -562,6 +571,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     // then a valid dual active-set iterate (KKT of the sub-problem, u >= 0), so the
     // method's convergence argument is unchanged; otherwise p takes the usual step.
     if (p2 >= 0) {
+      CNT(3);
       double zs2[CPL];
 #pragma unroll
       for (int k = 0; k < CPL; ++k) zs2[k] = cdot(vz2, k);
@@ -656,6 +666,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
           }
         }
         p = -1;
+        CNT(15);
         ++it;   // a pair step counts as the two additions it makes
         SEC(0);
         continue;
@@ -766,6 +777,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         aR[r] = -yv4[r] * ie;    // R -= y R_l / eta
       }
       zrow = l;
+      CNT(14);
 #pragma unroll
       for (int k = 0; k < VPL; ++k) u[k] = (lane + LANES * k == l) ? 0.0 : u[k];
       occ[l >> 6] &= ~(1ull << (l & 63));
@@ -827,7 +839,15 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   if (tid == 0 && Ug) {
     unsigned long long* dst = (unsigned long long*)(Ug + (size_t)b * N * 12);
     for (int i = 0; i < 7; ++i) dst[i] = stamps_[i];
-    for (int i = 0; i < 16; ++i) dst[8 + i] = secacc_[i];
+  }
+  fsync<NT>();
+  if (lane < 16 && Ug && 26 + 16 * (NT / LANES - 1) < N * 6) {   // per-wave section accumulators
+    unsigned long long* dst = (unsigned long long*)(Ug + (size_t)b * N * 12);
+    dst[(wave == 0 ? 8 : 10 + 16 * wave) + lane] = secacc_;
+  }
+  if (lane == 0 && Ug && 24 + wave < N * 6) {   // HW_ID of each wave (SIMD, CU, SE)
+    unsigned long long* dst = (unsigned long long*)(Ug + (size_t)b * N * 12);
+    dst[24 + wave] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
   }
   Ug = nullptr;
 #endif

@@ -56,13 +56,31 @@ def main():
     sel = iters > 0
     print(f"  active-set cycles / iteration: median {np.median(gi[sel] / iters[sel]):.0f}")
     sec = U.cpu().numpy().reshape(B, -1).view(np.uint64)[:, 8:24].astype(np.int64)
-    names = ["argmin p + a_p rows", "barrier", "zs = A z (LDS)", "-", "-", "add: q, 1/s, loads, coefs",
-             "drop: R_l, H R_l, R H R_l", "-", "pair candidate", "combo + LDS store", "pair-step test",
+    sec1 = U.cpu().numpy().reshape(B, -1).view(np.uint64)[:, 26:42].astype(np.int64)
+    # section k runs from SEC(k) to the next SEC (mpcqp_solve.h)
+    names = ["argmin p + a_p rows", "combo + LDS store", "zs = A z (LDS)", "-", "-", "add: q, 1/s, loads, coefs",
+             "drop: R_l, H R_l, R H R_l", "-", "pair candidate", "barrier", "pair-step test",
              "ratio test (loads, div, argmin)", "t2, step, x/u/s", "rank-1 FMAs (P, R)", "-", "-"]
+    # event counters (slots 3, 4, 14, 15): pair tests, fresh row choices, drops, pair steps
+    cnt = {"pair tests": sec[:, 3], "fresh choices": sec[:, 4], "drops": sec[:, 14], "pair steps": sec[:, 15]}
+    for k, v in cnt.items():
+        print(f"  count {k:14s} mean {v[sel].mean():6.1f}  max {v.max():4d}")
+    hw = U.cpu().numpy().reshape(B, -1).view(np.uint64)[:, 24:26].astype(np.int64)
+    simd = (hw >> 4) & 3
+    cu = ((hw >> 8) & 15) | (((hw >> 13) & 7) << 4)
+    print(f"  waves 0/1 on the same SIMD: {(simd[:, 0] == simd[:, 1]).mean():.3f}  same CU: "
+          f"{(cu[:, 0] == cu[:, 1]).mean():.3f}  raw {hw[:2].tolist()}")
+    print("  iteration histogram:", np.histogram(iters, bins=[0, 10, 20, 30, 40, 50, 60, 80, 200])[0].tolist())
+    for i in np.argsort(tot)[-6:]:
+        print(f"  robot {i}: it {iters[i]} fresh {sec[i, 4]} pair tests {sec[i, 3]} pairs {sec[i, 15]} "
+              f"drops {sec[i, 14]} loop cycles {dts[i, 3]} per pass {dts[i, 3] / max(1, iters[i] - sec[i, 15]):.0f}")
+        print("     sections:", {names[k]: int(sec[i, k]) for k in range(16) if names[k] != "-"})
+        print("     wave 1:  ", {names[k]: int(sec1[i, k]) for k in range(16) if names[k] != "-"})
     tot_it = iters[sel].sum()
     for k, name in enumerate(names):
         if name != "-":
-            print(f"  sec {name:20s} cycles/iteration (batch mean) {sec[sel, k].sum() / tot_it:8.0f}")
+            print(f"  sec {name:20s} cycles/iteration (batch mean) {sec[sel, k].sum() / tot_it:8.0f}"
+                  f"   wave 1 {sec1[sel, k].sum() / tot_it:8.0f}")
 
 
 if __name__ == "__main__":
