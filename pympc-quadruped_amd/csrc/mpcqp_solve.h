@@ -267,8 +267,8 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   // ------------------------------------------------ W = H^-1 (symmetric sweep)
   // pivot K = 8 KT + KC: W_ij -= z_i z_j / d, W_iK = z_i / d, W_KK = -1/d (ends at
   // -H^-1; padding rows/columns >= n never change).  One generic rank-1 pass (the
-  // pivot row's coefficient made inv - 1 turns row K into z_j / d), then the pivot
-  // column and diagonal by masked FMAs -- no per-element selects.  KC compile-time
+  // pivot row's coefficient made inv - 1 turns row K into z_j / d, the pivot column's
+  // entry of row K made d - 1 turns column K into z_i / d), then the diagonal.  KC compile-time
   // (register column), KT a runtime loop so the code stays in the instruction cache.
 #pragma unroll 1
   for (int KT = 0; TW * KT < n; ++KT) {
@@ -289,7 +289,8 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         double zr[TW], zi[4];
         ldt<TW>(zr, zc, tc);
         ld4(zi, zc, tr);
-        const double inv = rcp_nr(zc[K]);
+        const double dK = zc[K];
+        const double inv = rcp_nr(dK);
         double beta[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) beta[r] = -zi[r] * inv;
@@ -299,20 +300,19 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
           for (int r = 0; r < 4; ++r) beta[r] = (tr == KR && r == KRR) ? inv - 1.0 : beta[r];
         }
+        // column K rides along in the same pass: with its row-K entry taken as d - 1,
+        // W_iK + beta_i (d - 1) = z_i - z_i (d - 1) / d = z_i / d, and the pivot
+        // entry becomes d + (1/d - 1)(d - 1) = 2 - 1/d (-> -1/d below)
+        if (tc == KT) zr[KC] = dK - 1.0;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
           for (int c = 0; c < TW; ++c) W[r][c] = fma(beta[r], zr[c], W[r][c]);
-        // column K: the pass left z_i - z_i d/d ~ 0 there; add z_i / d.  Diagonal:
-        // d/d + 1 -> -1/d.
-        const double cm = (tc == KT) ? inv : 0.0;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) W[r][KC] = fma(zi[r], cm, W[r][KC]);
         if constexpr (TW == 8) {
-          W[KC & 3][KC] += (tc == KT && tr == KR) ? -inv - 2.0 : 0.0;
+          W[KC & 3][KC] += (tc == KT && tr == KR) ? -2.0 : 0.0;
         } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) W[r][KC] += (tc == KT && tr == KR && r == KRR) ? -inv - 2.0 : 0.0;
+          for (int r = 0; r < 4; ++r) W[r][KC] += (tc == KT && tr == KR && r == KRR) ? -2.0 : 0.0;
         }
       }
     });
