@@ -80,31 +80,43 @@ template <int NT>
 __device__ __forceinline__ bool form_stage(Form& f, int N, int b, int tid, const float* __restrict__ x0g,
                                            const float* __restrict__ xrefg, const float* __restrict__ contactg,
                                            const float* __restrict__ feetg, const float* __restrict__ robotg) {
+  // The robot's five input slices, staged into LDS with 16-byte loads: each slice is
+  // covered by the 16-byte-aligned chunks that hold it (a chunk never crosses a page,
+  // so the few bytes of the neighbouring robots it also holds are always readable),
+  // and a lane stores the chunk's floats that fall inside the slice.
   float* const in = f.in;
-  const float* xb = x0g + (size_t)b * NX;
-  const float* fb = feetg + (size_t)b * 12;
-  const float* rb = robotg + (size_t)b * MPCQP_ROBOT_STRIDE;
-  const float* cb = contactg + (size_t)b * N * 4;
-  const float* xrb = xrefg + (size_t)b * N * NX;
+  // slices: x0, feet, robot record, contact, xref (no runtime-indexed private
+  // arrays below: those would live in scratch)
+  const float* const p0 = x0g + (size_t)b * NX;
+  const float* const p1 = feetg + (size_t)b * 12;
+  const float* const p2 = robotg + (size_t)b * MPCQP_ROBOT_STRIDE;
+  const float* const p3 = contactg + (size_t)b * N * 4;
+  const float* const p4 = xrefg + (size_t)b * N * NX;
+  auto nchunks = [](const float* q, int len) -> int {
+    const uintptr_t a = (uintptr_t)q;
+    return (int)(((a + 4 * (uintptr_t)len + 15) >> 4) - (a >> 4));
+  };
+  const int c1 = nchunks(p0, NX), c2 = c1 + nchunks(p1, 12), c3 = c2 + nchunks(p2, MPCQP_ROBOT_STRIDE),
+            c4 = c3 + nchunks(p3, 4 * N), c5 = c4 + nchunks(p4, NX * N);
   int bad = 0;
-  if (tid < NX) {
-    const float v = xb[tid];
-    in[IN_X0 + tid] = v;
-    bad |= !isfinite(v);
-  } else if (tid < NX + 12) {
-    const float v = fb[tid - NX];
-    in[IN_FEET + tid - NX] = v;
-    bad |= !isfinite(v);
-  } else if (tid < NX + 12 + MPCQP_ROBOT_STRIDE) {
-    const float v = rb[tid - NX - 12];
-    in[IN_ROBOT + tid - NX - 12] = v;
-    bad |= (tid < NX + 12 + 12) && !isfinite(v);
-  }
-  for (int k = tid; k < 4 * N; k += NT) in[IN_CONTACT + k] = cb[k];
-  for (int k = tid; k < NX * N; k += NT) {
-    const float v = xrb[k];
-    in[IN_XREF + k] = v;
-    bad |= !isfinite(v);
+  for (int c = tid; c < c5; c += NT) {
+    const int i = (c >= c1) + (c >= c2) + (c >= c3) + (c >= c4);
+    const float* const q = i == 0 ? p0 : i == 1 ? p1 : i == 2 ? p2 : i == 3 ? p3 : p4;
+    const int cb = i == 0 ? 0 : i == 1 ? c1 : i == 2 ? c2 : i == 3 ? c3 : c4;
+    const int len = i == 0 ? NX : i == 1 ? 12 : i == 2 ? 12 : i == 3 ? 4 * N : NX * N;   // robot: 12 fields read
+    const int dst = i == 0 ? IN_X0 : i == 1 ? IN_FEET : i == 2 ? IN_ROBOT : i == 3 ? IN_CONTACT : IN_XREF;
+    const uintptr_t base = ((uintptr_t)q & ~(uintptr_t)15) + 16 * (uintptr_t)(c - cb);
+    const float4 v = *reinterpret_cast<const float4*>(base);
+    const int e = (int)(((intptr_t)base - (intptr_t)q) >> 2);   // slice index of v.x (may be < 0)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float w = j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
+      const int k = e + j;
+      if (k >= 0 && k < len) {
+        in[dst + k] = w;
+        bad |= i != 3 && !isfinite(w);   // contact is not checked
+      }
+    }
   }
   return !fany<NT>(bad != 0);
 }
