@@ -507,7 +507,7 @@ def main():
                        "batch_per_gpu": Bpg, "horizon": N, "global_batch": world * Bpg,
                        "parallelism": f"robot-sharded x{world}" + gather_label},
             # the governing pipe is the FP64 vector ALU (VALU): no MFMA instruction is on
-            # the path (gfx950's FP64 MFMA peak equals its FP64 VALU peak, DESIGN §4.4)
+            # the path (gfx950's FP64 MFMA peak equals its FP64 VALU peak, DESIGN §4.5)
             "roofline": {"bound": "valu", "pipe": "fp64 VALU", "achieved": achieved, "peak": PEAK_FP64_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic,
                          "executed_frac": E_avg / kavg_s / 1e12 / PEAK_FP64_TFLOPS},

@@ -4,9 +4,9 @@ Copies the kernel-trace stats CSV and derives, for the engine kernel, the
 average dispatch duration and HBM traffic per launch from the PMC passes:
   FETCH_SIZE, WRITE_SIZE are in KiB per dispatch (rocprofv3, gfx950).
   MI355X_MICROARCH.md §HBM: FETCH_SIZE reads exactly 1/2 of the bytes of a wide
-  (16 B/lane) coalesced stream; other widths are uncalibrated.  The engine's
-  loads are 4-B-per-lane staging loads, so both the raw and the x2-corrected
-  read figures are reported.
+  (16 B/lane) coalesced stream; other widths are uncalibrated.  The QP kernels
+  stage their inputs with 16-B loads (mpcqp_form.h::form_stage), so the x2
+  correction applies to them; the raw figure is reported as well.
 """
 import csv
 import glob
@@ -80,7 +80,7 @@ def main():
         "kernel_ms_avg_bench_events": bench.get("kernel_ms_avg"),
         "hbm_bytes_per_launch": dom.get("hbm_bytes_per_launch"),
         "kernels": per_kernel,
-        "note": "FETCH_SIZE x2 per MI355X_MICROARCH.md (wide-stream calibration; 4-B staging loads are uncalibrated)",
+        "note": "FETCH_SIZE x2 per MI355X_MICROARCH.md (16-B/lane stream calibration; the QP kernels stage inputs with 16-B loads)",
     }
     path = os.path.join(dst, "pmc_traffic.json")
     data = {}
