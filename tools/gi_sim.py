@@ -53,7 +53,7 @@ def robot_qp(bt, b, N):
     return H, g, np.array(A), np.array(bb), np.array(foot)
 
 
-def simulate(H, g, A, b, foot, kmax, tol=1e-9, max_pass=2000):
+def simulate(H, g, A, b, foot, kmax, tol=1e-9, max_pass=2000, ratio=0.0, stop_after_drops=10**9):
     n = H.shape[0]
     W = np.linalg.inv(H)
     P = W.copy()
@@ -78,11 +78,14 @@ def simulate(H, g, A, b, foot, kmax, tol=1e-9, max_pass=2000):
             cands = []
             used = set()
             order = np.argsort(key, kind="stable")
+            klim = kmax if drops < stop_after_drops else 1
             for c in order:
-                if not np.isfinite(key[c]) or len(cands) >= kmax:
+                if not np.isfinite(key[c]) or len(cands) >= klim:
                     break
                 if foot[c] in used:
                     continue
+                if cands and key[c] > ratio * key[cands[0]]:   # partners at least `ratio` as violated
+                    break
                 cands.append(c)
                 used.add(foot[c])
             p = cands[0]
@@ -176,13 +179,16 @@ def simulate(H, g, A, b, foot, kmax, tol=1e-9, max_pass=2000):
 
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
-    ks = [int(a) for a in sys.argv[2:]] or [1, 2, 3, 4]
+    ks = [a for a in sys.argv[2:]] or ["1", "2", "3", "4"]
     N = 10
     bt = make_batch(B, N, seed=1000, gaits=("trot10",), robots=("a1",))
     qps = [robot_qp(bt, b, N) for b in range(B)]
     ref = None
-    for k in ks:
-        res = [simulate(*qp, kmax=k) for qp in qps]
+    for ka in ks:
+        parts = ka.split(":")   # "k", "k:ratio" or "k:ratio:drops"
+        k, r = int(parts[0]), float(parts[1]) if len(parts) > 1 else 0.0
+        sd = int(parts[2]) if len(parts) > 2 else 10**9
+        res = [simulate(*qp, kmax=k, ratio=r, stop_after_drops=sd) for qp in qps]
         passes = np.array([r["passes"] for r in res])
         its = np.array([r["it"] for r in res])
         drops = np.array([r["drops"] for r in res])
@@ -191,7 +197,7 @@ def main():
         cost = np.array([r["cost"] for r in res])
         dev = max(np.abs(r["x"] - x0).max() / max(np.abs(x0).max(), 1e-3) for r, x0 in zip(res, ref))
         top = np.argsort(passes)[-5:]
-        print(f"k={k}: passes mean {passes.mean():.1f} max {passes.max()} | it mean {its.mean():.1f} max {its.max()}"
+        print(f"k={ka}: passes mean {passes.mean():.1f} max {passes.max()} | it mean {its.mean():.1f} max {its.max()}"
               f" | drops mean {drops.mean():.2f} max {drops.max()} | x dev vs k={ks[0]} {dev:.1e}"
               f" | cost mean {cost.mean():.1f} max {cost.max():.1f}"
               f" | slowest {[(int(i), int(passes[i]), int(its[i]), int(drops[i])) for i in top]}")
