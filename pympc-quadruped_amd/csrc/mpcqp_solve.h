@@ -265,6 +265,93 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   STAMP(2);
 
   // ------------------------------------------------ W = H^-1 (symmetric sweep)
+  if constexpr (NV >= 96) {
+  // Classes 96 / 128 (one robot per CU, latency-bound; 6- / 8-wave barriers):
+  // pivot PAIRS {K, K + 1} (K even: one tile column, one 4-row group; K + 1 = n is
+  // the decoupled identity padding when n is odd).  With Z = W[:, {K, K+1}] and its
+  // pivot block D, the block sweep W_ij -= (Z D^-1)_i . Z_j, W_iK = (Z D^-1)_i,
+  // W_KK = -D^-1 is ONE rank-2 pass: coefficient rows -(Z D^-1)_i (pivot rows:
+  // (D^-1 - I)_a, turning rows K into D^-1 Z^T), the pair's columns entering with
+  // D - I in place of D (turning columns K into Z D^-1), then -2 on the pivot
+  // diagonal.  Half the barriers and pivot-column round trips of single pivots;
+  // class 64 (four robots per CU, issue-bound when they sweep together) keeps
+  // single pivots, which issue fewer instructions.  The pair's two columns are
+  // double-buffered by pair parity in the zc / vz space.
+#pragma unroll 1
+  for (int KT = 0; TW * KT < n; ++KT) {
+    static_for<TW / 2>([&](auto KPc) {
+      constexpr int KC = 2 * decltype(KPc)::value;
+      const int K = TW * KT + KC;
+      const int KR = TW == 8 ? 2 * KT + (KC >> 2) : K >> 2;
+      const int KRR = TW == 8 ? (KC & 3) : (K & 3);   // 0 or 2
+      if (K < n) {
+        double* const z0 = sm.zc[0] + ((K >> 1) & 1) * (2 * C::VEC);
+        double* const z1 = z0 + C::VEC;
+        if (tc == KT) {
+          d2* q0 = reinterpret_cast<d2*>(z0 + 4 * tr);
+          q0[0] = d2{W[0][KC], W[1][KC]};
+          q0[1] = d2{W[2][KC], W[3][KC]};
+          d2* q1 = reinterpret_cast<d2*>(z1 + 4 * tr);
+          q1[0] = d2{W[0][KC + 1], W[1][KC + 1]};
+          q1[1] = d2{W[2][KC + 1], W[3][KC + 1]};
+        }
+        fsync<NT>();
+        double zr0[TW], zr1[TW], zi0[4], zi1[4];
+        ldt<TW>(zr0, z0, tc);
+        ldt<TW>(zr1, z1, tc);
+        ld4(zi0, z0, tr);
+        ld4(zi1, z1, tr);
+        const double d00 = z0[K], d01 = z0[K + 1], d11 = z1[K + 1];
+        const double idet = rcp_nr(fma(d00, d11, -d01 * d01));
+        const double e00 = d11 * idet, e01 = -d01 * idet, e11 = d00 * idet;   // D^-1
+        double c0[4], c1[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          c0[r] = -fma(zi0[r], e00, zi1[r] * e01);
+          c1[r] = -fma(zi0[r], e01, zi1[r] * e11);
+        }
+        if constexpr (TW == 8) {
+          if (tr == KR) {
+            c0[KRR] = e00 - 1.0;
+            c1[KRR] = e01;
+            c0[KRR + 1] = e01;
+            c1[KRR + 1] = e11 - 1.0;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; r += 2) {
+            const bool at = tr == KR && r == KRR;
+            c0[r] = at ? e00 - 1.0 : c0[r];
+            c1[r] = at ? e01 : c1[r];
+            c0[r + 1] = at ? e01 : c0[r + 1];
+            c1[r + 1] = at ? e11 - 1.0 : c1[r + 1];
+          }
+        }
+        if (tc == KT) {   // the pair's columns enter with D - I
+          zr0[KC] -= 1.0;
+          zr1[KC + 1] -= 1.0;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int c = 0; c < TW; ++c) W[r][c] = fma(c1[r], zr1[c], fma(c0[r], zr0[c], W[r][c]));
+        if constexpr (TW == 8) {
+          if (tc == KT && tr == KR) {
+            W[KRR][KC] -= 2.0;
+            W[KRR + 1][KC + 1] -= 2.0;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; r += 2) {
+            const bool at = tc == KT && tr == KR && r == KRR;
+            W[r][KC] -= at ? 2.0 : 0.0;
+            W[r + 1][KC + 1] -= at ? 2.0 : 0.0;
+          }
+        }
+      }
+    });
+  }
+  } else {
   // pivot K = 8 KT + KC: W_ij -= z_i z_j / d, W_iK = z_i / d, W_KK = -1/d (ends at
   // -H^-1; padding rows/columns >= n never change).  One generic rank-1 pass (the
   // pivot row's coefficient made inv - 1 turns row K into z_j / d, the pivot column's
@@ -316,6 +403,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         }
       }
     });
+  }
   }
   // P = -(sweep result) = H^-1 ; largest diagonal entry (dependency threshold scale)
   double wd = 0.0;
