@@ -231,3 +231,33 @@ def test_two_streams_no_host_sync():
         for b in range(0, len(bt["x0"]), 7):
             x, _, _ = oracle_solution(bt, b, N)
             assert rel_err_u0(U[b], x) < TOL_U0, b
+
+
+@pytest.mark.parametrize("N", [10, 16, 20])
+def test_random_contact_patterns_every_class(N):
+    """Arbitrary (not gait-table) contact patterns with per-robot mu, fz_max and tilted
+    cone normals: stance counts from 0 to 4N, so one call routes robots to every
+    capacity class (64 / 96 / 128 and the interior-point class for n > 128 at
+    N = 16 / 20) -- each robot's u0 and U against the float64 oracle."""
+    from mpcqp.params import R_FZMAX, R_MU, R_NX, R_NZ
+    from mpcqp.synthetic import make_batch
+    B = 40
+    rng = np.random.default_rng(100 + N)
+    bt = make_batch(B, N, seed=200 + N, gaits=("trot10", "pace10", "bound8"), robots=("a1", "aliengo"),
+                    tilt_deg=20.0)
+    density = rng.uniform(0.05, 1.0, size=(B, 1, 1))
+    bt["contact"] = (rng.random((B, N, 4)) < density).astype(np.float32)
+    bt["contact"][0] = 1.0   # standing over the whole horizon (n = 12 N)
+    bt["contact"][1] = 0.0   # flight over the whole horizon (n = 0)
+    bt["robot"][:, R_MU] = rng.uniform(0.2, 1.0, B).astype(np.float32)
+    bt["robot"][:, R_FZMAX] = rng.uniform(120.0, 600.0, B).astype(np.float32)
+    u0, U, status, _ = _solve(_engine(N), bt)
+    assert (status == 0).all(), status
+    stance = bt["contact"].reshape(B, -1).sum(1)
+    assert stance.max() == 4 * N and stance.min() == 0
+    for b in range(B):
+        x, _, _ = oracle_solution(bt, b, N)
+        assert rel_err_u0(u0[b], x[:12]) < TOL_U0, (b, int(stance[b]), u0[b], x[:12])
+        assert rel_err_u0(U[b], x) < TOL_U0, (b, int(stance[b]))
+    assert np.all(U[1] == 0) and np.all(u0[1] == 0)
+    assert bt["robot"][:, R_NX:R_NZ + 1].shape == (B, 3)
