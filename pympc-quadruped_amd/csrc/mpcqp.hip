@@ -43,6 +43,9 @@ constexpr int kMaxN = 20;   // LDS scratch is sized for N <= 20
 #ifndef MPCQP_C64_TW
 #define MPCQP_C64_TW 8   // class-64 register tile width (8: 2 waves per robot; 4: 4 waves, slower)
 #endif
+#ifndef MPCQP_SWEEP_MFMA
+#define MPCQP_SWEEP_MFMA 0   // 1: class-64 H^-1 sweep blocked by 4 pivots on the f64 MFMA (parity-exact, slower: DESIGN 4.5)
+#endif
 #ifndef MPCQP_C64_WPE
 #define MPCQP_C64_WPE (MPCQP_C64_TW == 4 ? 4 : 2)   // class-64 waves per SIMD (VGPR budget)
 #endif
@@ -291,6 +294,7 @@ __device__ __forceinline__ int wave_argmin_f32(double v, double& vmin_out) {
 }
 
 #include "mpcqp_form.h"
+#include "mpcqp_sweep_mfma.h"
 #include "mpcqp_solve.h"
 #include "mpcqp_ipm.h"
 #include "mpcqp_plan.h"

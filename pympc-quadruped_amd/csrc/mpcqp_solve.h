@@ -255,8 +255,9 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
     for (int r = 0; r < 4; ++r) hrow(r, cj, cc, W[r]);   // unrolled: rows land in their registers
   }
-  {
-    fsync<NT>();   // every lane is done reading the formulation scratch H overwrites
+  constexpr bool kMfmaSweep = NV == 64 && MPCQP_SWEEP_MFMA;
+  fsync<NT>();   // every lane is done reading the formulation scratch H overwrites
+  if constexpr (!kMfmaSweep) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -265,7 +266,19 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   STAMP(2);
 
   // ------------------------------------------------ W = H^-1 (symmetric sweep)
-  if constexpr (NV >= 96) {
+  if constexpr (kMfmaSweep) {
+    // class 64: blocked by 4 pivots on the f64 matrix cores (mpcqp_sweep_mfma.h),
+    // in the LDS of the H copy, which is stored afterwards
+    double Ws[4][TW];
+    sweep_mfma64(W, Ws, sm.ht, n, tid);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < TW; ++c) {
+        sm.ht[(TW * r + c) * NT + tid] = W[r][c];
+        W[r][c] = Ws[r][c];
+      }
+  } else if constexpr (NV >= 96) {
   // Classes 96 / 128 (one robot per CU, latency-bound; 6- / 8-wave barriers):
   // pivot PAIRS {K, K + 1} (K even: one tile column, one 4-row group; K + 1 = n is
   // the decoupled identity padding when n is odd).  With Z = W[:, {K, K+1}] and its

@@ -53,9 +53,9 @@ def robot_qp(bt, b, N):
     return H, g, np.array(A), np.array(bb), np.array(foot)
 
 
-def simulate(H, g, A, b, foot, kmax, tol=1e-9, max_pass=2000, ratio=0.0, stop_after_drops=10**9):
+def simulate(H, g, A, b, foot, kmax, tol=1e-9, max_pass=2000, ratio=0.0, stop_after_drops=10**9, W0=None):
     n = H.shape[0]
-    W = np.linalg.inv(H)
+    W = np.linalg.inv(H) if W0 is None else W0.copy()
     P = W.copy()
     R = np.zeros((n, n))          # slot rows
     occ = np.zeros(n, bool)
