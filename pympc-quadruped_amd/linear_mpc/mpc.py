@@ -103,36 +103,75 @@ class ModelPredictiveController():
                           Q=self.q_diag, R=self.r_diag, device=os.environ.get("MPCQP_DEVICE", "cuda:0"))
             e.set_planner(dt_control=self.dt_control, gravity=self.gravity)
             d, f32 = e.device, dict(dtype=torch.float32, device=e.device)
+            N = self.horizon
             self._dev = dict(
                 plan_state=torch.zeros((1, PLAN_STRIDE), dtype=torch.float64, device=d),
-                x0=torch.zeros((1, 13), **f32), xref=torch.zeros((1, self.horizon, 13), **f32),
-                xref_gen=torch.zeros((1, self.horizon, 13), **f32),
+                x0=torch.zeros((1, 13), **f32), xref=torch.zeros((1, N, 13), **f32),
+                xref_gen=torch.zeros((1, N, 13), **f32),
                 height=torch.full((1,), float(self.com_height_des), **f32),
-                robot=torch.as_tensor(self._robot_record).reshape(1, -1).to(d))
+                robot=torch.as_tensor(self._robot_record).reshape(1, -1).to(d),
+                u0=torch.zeros((1, 12), **f32),
+                # solve outputs in one buffer: U [12N] f32, status and iterations as int32
+                # bits -- one device->host copy per MPC tick
+                out=torch.zeros((12 * N + 2,), **f32))
+            self._dev["U"] = self._dev["out"][:12 * N]
+            self._dev["status"] = self._dev["out"][12 * N:12 * N + 1].view(torch.int32)
+            self._dev["iters"] = self._dev["out"][12 * N + 1:].view(torch.int32)
+            # one host->device upload per control iteration (byte offsets, 8-aligned):
+            # [0, 24) v_des body f64[3], [24, 32) yaw rate f64, [32, 120) the planner's
+            # float32 state (quat, pos, omega, vel, R_base), [128, ...) on MPC ticks the
+            # gait table f32[4N] and the feet f32[12]
+            self._up_bytes = 128 + 4 * (4 * N + 12)
+            self._up_host = np.zeros(self._up_bytes, dtype=np.uint8)
+            self._up_dev = torch.zeros((self._up_bytes,), dtype=torch.uint8, device=d)
             self._engine = e
         return self._engine
 
-    def _planner_inputs(self):
-        """robot_data -> the planner's device inputs (float32 state, float32 R_base)."""
+    def _upload(self, vel_base_des_body, yaw_turn_rate, gait_table=None):
+        """Pack the iteration's host inputs (and on MPC ticks the gait table and foot
+        positions) into one buffer and copy it to the device in one transfer."""
         import torch
-        rd = self.__robot_data
-        d = self._engine.device
-        host = np.concatenate([np.asarray(rd.quat_base, dtype=np.float32).reshape(4),
-                               np.asarray(rd.pos_base, dtype=np.float32).reshape(3),
-                               np.asarray(rd.ang_vel_base, dtype=np.float32).reshape(3),
-                               np.asarray(rd.lin_vel_base, dtype=np.float32).reshape(3),
-                               np.asarray(rd.R_base, dtype=np.float32).reshape(9)])
-        t = torch.from_numpy(host).to(d)
-        return dict(quat=t[0:4], pos=t[4:7], omega=t[7:10], vel=t[10:13], rot=t[13:22])
+        h = self._up_host
+        lo, nbytes = 0, 120
+        if vel_base_des_body is None:   # gait table and feet only (a direct _solve_mpc call)
+            lo = 128
+        else:
+            rd = self.__robot_data
+            h[0:24].view(np.float64)[:] = np.asarray(vel_base_des_body, dtype=np.float64).reshape(3)
+            h[24:32].view(np.float64)[0] = float(yaw_turn_rate)
+            f = h[32:120].view(np.float32)
+            f[0:4] = np.asarray(rd.quat_base, dtype=np.float32).reshape(4)
+            f[4:7] = np.asarray(rd.pos_base, dtype=np.float32).reshape(3)
+            f[7:10] = np.asarray(rd.ang_vel_base, dtype=np.float32).reshape(3)
+            f[10:13] = np.asarray(rd.lin_vel_base, dtype=np.float32).reshape(3)
+            f[13:22] = np.asarray(rd.R_base, dtype=np.float32).reshape(9)
+        if gait_table is not None:
+            nt = 4 * self.horizon
+            g = h[128:self._up_bytes].view(np.float32)
+            g[:nt] = np.asarray(gait_table, dtype=np.float32).reshape(-1)
+            g[nt:nt + 12] = self._feet_host()
+            nbytes = self._up_bytes
+        dev = self._up_dev
+        dev[lo:nbytes].copy_(torch.from_numpy(h[lo:nbytes]))
+        fd = dev[32:120].view(torch.float32)
+        v = dict(vb=dev[0:24].view(torch.float64).reshape(1, 3), yr=dev[24:32].view(torch.float64),
+                 quat=fd[0:4], pos=fd[4:7], omega=fd[7:10], vel=fd[10:13], rot=fd[13:22])
+        if gait_table is not None:
+            g = dev[128:self._up_bytes].view(torch.float32)
+            v["contact"] = g[:4 * self.horizon].reshape(1, -1)
+            v["feet"] = g[4 * self.horizon:].reshape(1, 4, 3)
+            v["stance"] = int(np.count_nonzero(h[128:128 + 16 * self.horizon].view(np.float32) > 0))
+        return v
 
-    def _plan(self, flags, vel_base_des_body, yaw_turn_rate, xref_key="xref"):
-        import torch
+    def _feet_host(self):
+        return np.asarray([np.asarray(f, dtype=np.float64).reshape(3) for f in self.pos_base_feet],
+                          dtype=np.float32).reshape(-1)
+
+    def _plan(self, flags, up, xref_key="xref"):
         e = self._get_engine()
         dv = self._dev
-        vb = torch.as_tensor(np.asarray(vel_base_des_body, dtype=np.float64).reshape(1, 3)).to(e.device)
-        yr = torch.full((1,), float(yaw_turn_rate), dtype=torch.float64, device=e.device)
-        e.plan(flags, dv["plan_state"], dv["x0"], vb, yr, height_des=dv["height"], xref=dv[xref_key],
-               **self._planner_inputs())
+        e.plan(flags, dv["plan_state"], dv["x0"], up["vb"], up["yr"], height_des=dv["height"], xref=dv[xref_key],
+               quat=up["quat"], pos=up["pos"], omega=up["omega"], vel=up["vel"], rot=up["rot"])
 
     def _planner_state(self):
         return self._dev["plan_state"].cpu().numpy()[0]
@@ -174,16 +213,20 @@ class ModelPredictiveController():
         """mpc.py:81-108: integrators on the device every call, a solve on MPC ticks."""
         from mpcqp._lib import PLAN_REFERENCE
         self._base_vel_base_des = np.asarray(base_vel_base_des, dtype=np.float64).reshape(3)
+        self._get_engine()
         if iter_counter % self.iterations_between_mpc == 0:
-            # integrate + reference trajectory in one launch (mpc.py:84-92, :110-170)
-            self._plan(PLAN_REFERENCE, self._base_vel_base_des, yaw_turn_rate_des)
+            assert solver == 'drake' or solver == 'qpsolvers' or solver == 'hip'
+            # one upload (state, command, gait table, feet), integrate + reference
+            # trajectory in one launch (mpc.py:84-92, :110-170), then the solve
+            up = self._upload(self._base_vel_base_des, yaw_turn_rate_des, gait_table)
+            self._plan(PLAN_REFERENCE, up)
             self.is_first_run = False
-            self.__contact_forces = self._solve_mpc(self._dev["xref"], gait_table, solver=solver)[0:12]
+            self.__contact_forces = self._solve_dev(up["contact"], up["feet"], up["stance"])[0:12]
             self._ref_traj_host = None   # ref_traj (mpc.py:97) is read back only when asked for
             if debug and iter_counter == iter_debug:
                 warnings.warn("debug CoM-trajectory plot (mpc.py:293-318) is not provided by the engine")
         else:
-            self._plan(0, self._base_vel_base_des, yaw_turn_rate_des)
+            self._plan(0, self._upload(self._base_vel_base_des, yaw_turn_rate_des))
             self.is_first_run = False
         return self.__contact_forces[0:12]
 
@@ -203,7 +246,8 @@ class ModelPredictiveController():
         R = np.asarray(self.__robot_data.R_base, dtype=np.float64).reshape(3, 3)
         vb = np.linalg.solve(R, np.asarray(vel_base_des, dtype=np.float64).reshape(3))
         # its own X_ref buffer: ref_traj keeps the last MPC tick's (mpc.py:96-97)
-        self._plan(PLAN_REFERENCE | PLAN_NO_INTEGRATE, vb, yaw_turn_rate, xref_key="xref_gen")
+        self._get_engine()
+        self._plan(PLAN_REFERENCE | PLAN_NO_INTEGRATE, self._upload(vb, yaw_turn_rate), xref_key="xref_gen")
         return self._dev["xref_gen"].cpu().numpy().reshape(-1)
 
     def _solve_mpc(self, ref_traj, gait_table, solver='drake', debug=False):
@@ -214,23 +258,24 @@ class ModelPredictiveController():
         assert solver == 'drake' or solver == 'qpsolvers' or solver == 'hip'
         import torch
         e = self._get_engine()
-        table = np.asarray(gait_table, dtype=np.float32).reshape(-1)
-        feet = np.asarray([np.asarray(f, dtype=np.float64).reshape(3) for f in self.pos_base_feet],
-                          dtype=np.float32).reshape(-1)
-        # one host->device copy for the gait table and the foot positions
-        hostin = torch.from_numpy(np.concatenate([table, feet]))
-        devin = hostin.to(e.device, non_blocking=False)
-        # the exact stance count of this table: the engine launches only the capacity
-        # classes it can need
-        e.set_stance_hint(int(np.count_nonzero(table > 0)))
-        res = e.solve(self._dev["x0"], ref_traj if not isinstance(ref_traj, np.ndarray)
-                      else np.asarray(ref_traj, dtype=np.float32)[None, :],
-                      devin[:table.size].reshape(1, -1), devin[table.size:].reshape(1, 4, 3),
-                      robot=self._dev["robot"], return_all=True)
-        # one device->host copy (and one synchronisation) for U and the status
-        out = torch.cat([res.U.reshape(-1), res.status.to(torch.float32)]).cpu().numpy()
-        U = out[:-1].astype(np.float64)
-        status = int(out[-1])
+        up = self._upload(None, 0.0, gait_table)
+        xr = ref_traj if isinstance(ref_traj, torch.Tensor) else \
+            torch.from_numpy(np.asarray(ref_traj, dtype=np.float32).reshape(1, self.horizon, 13)).to(e.device)
+        return self._solve_dev(up["contact"], up["feet"], up["stance"], xr.reshape(1, self.horizon, 13))
+
+    def _solve_dev(self, contact, feet, stance, xref=None):
+        """The engine call on device buffers: preallocated outputs, one device->host
+        copy (and one synchronisation) for U and the status."""
+        e = self._engine
+        dv = self._dev
+        # the exact stance count of this table: only the capacity classes it needs launch
+        e.set_stance_hint(stance)
+        e.solve_raw(1, dv["x0"], dv["xref"] if xref is None else xref, contact, feet, dv["robot"], dv["u0"],
+                    dv["U"], dv["status"], dv["iters"])
+        out = dv["out"].cpu().numpy()
+        N12 = 12 * self.horizon
+        U = out[:N12].astype(np.float64)
+        status = int(out[N12:N12 + 1].view(np.int32)[0])
         if status == 3 or status == 4:   # MPCQP_STATUS_TOO_LARGE / NONFINITE: no usable forces
             raise RuntimeError(f"mpcqp: robot solve failed with status {status}")
         if status != 0:
