@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define MPCQP_ABI_VERSION 2
+#define MPCQP_ABI_VERSION 3
 #define MPCQP_ROBOT_STRIDE 16
 #define MPCQP_MAX_HORIZON 32
 
@@ -92,6 +92,13 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
 /* Largest number of stance foot-steps the caller promises per robot
  * (0 = unknown: the engine dispatches every capacity class). */
 int mpcqp_set_stance_hint(mpcqp_ctx* ctx, int32_t max_stance);
+
+/* Both bounds on the stance foot-steps per robot (min 0 and max 0 = no promise):
+ * classes no robot can need are not launched, and when the range rules out the
+ * smaller classes the first possible one takes the batch directly (the drop-in
+ * controller passes its gait table's exact count).  A robot outside the range is
+ * still solved if a launched class covers it, else reports MPCQP_STATUS_TOO_LARGE. */
+int mpcqp_set_stance_range(mpcqp_ctx* ctx, int32_t min_stance, int32_t max_stance);
 
 /* ---- the hot path's callers on the device -------------
  *

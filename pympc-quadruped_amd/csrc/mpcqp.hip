@@ -333,14 +333,19 @@ __global__ __launch_bounds__(Cfg<96>::NT) __attribute__((amdgpu_waves_per_eu(2, 
     KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
-    int* __restrict__ queue, int* __restrict__ qout) {
+    int* __restrict__ queue, int* __restrict__ qout, int* __restrict__ q_ipm, int direct_B) {
   __shared__ SharedT<96> sm;
   const int tid = threadIdx.x;
   const int k = blockIdx.x;
+  if (direct_B > 0) {   // the caller's stance range rules class 64 out: robot = workgroup
+    if (k < direct_B) solve_robot<96>(P, k, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, qout,
+                                      nullptr, q_ipm);
+    return;
+  }
   const int cnt = uni(__hip_atomic_load(&queue[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (k < cnt) {
     const int b = uni(queue[4 + k]);
-    solve_robot<96>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, qout);
+    solve_robot<96>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, qout, nullptr, q_ipm);
     // only the cnt workers count themselves (no contended atomic from the idle rest)
     if (tid == 0 && atomicAdd(&queue[2], 1) == cnt - 1) {
       atomicExch(&queue[0], 0);
@@ -359,14 +364,19 @@ __global__ __launch_bounds__(Cfg<128>::NT) void mpcqp_kernel_128(
     KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
-    int* __restrict__ queue) {
+    int* __restrict__ queue, int* __restrict__ q_ipm, int direct_B) {
   __shared__ SharedT<128> sm;
   const int tid = threadIdx.x;
   const int k = blockIdx.x;
+  if (direct_B > 0) {
+    if (k < direct_B) solve_robot<128>(P, k, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg,
+                                       q_ipm, nullptr, q_ipm);
+    return;
+  }
   const int cnt = uni(__hip_atomic_load(&queue[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (k < cnt) {
     const int b = uni(queue[4 + k]);
-    solve_robot<128>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, nullptr);
+    solve_robot<128>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, q_ipm, nullptr, q_ipm);
     // only the cnt workers count themselves (no contended atomic from the idle rest)
     if (tid == 0 && atomicAdd(&queue[2], 1) == cnt - 1) {
       atomicExch(&queue[0], 0);
@@ -382,10 +392,14 @@ __global__ __launch_bounds__(LANES) void mpcqp_kernel_ipm(
     KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
-    int* __restrict__ queue) {
+    int* __restrict__ queue, int direct_B) {
   __shared__ IpmShared sm;
   const int tid = threadIdx.x;
   const int k = blockIdx.x;
+  if (direct_B > 0) {
+    if (k < direct_B) solve_robot_ipm(P, k, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg);
+    return;
+  }
   const int cnt = uni(__hip_atomic_load(&queue[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (k < cnt) {
     const int b = uni(queue[4 + k]);
@@ -413,7 +427,8 @@ struct QueueSet {
 struct mpcqp_ctx {
   mpcqp_params params;
   int device;
-  int stance_hint;
+  int stance_hint;   // max stance foot-steps per robot promised by the caller (0: none)
+  int stance_min;    // min stance foot-steps per robot promised by the caller
   int ncu;
   std::vector<QueueSet> queues;
   double dt_control;  // planner constants (mpcqp_set_planner)
@@ -506,6 +521,7 @@ int mpcqp_create(const mpcqp_params* p, int32_t device, mpcqp_ctx** out) {
   ctx->params = *p;
   ctx->device = device;
   ctx->stance_hint = 0;
+  ctx->stance_min = 0;
   ctx->ncu = 0;
   ctx->dt_control = 0.001;    // linear_mpc_configs.py:6
   ctx->gravity = 9.81;        // linear_mpc_configs.py:13
@@ -518,7 +534,12 @@ int mpcqp_create(const mpcqp_params* p, int32_t device, mpcqp_ctx** out) {
 }
 
 int mpcqp_set_stance_hint(mpcqp_ctx* ctx, int32_t max_stance) {
-  if (!ctx || max_stance < 0) return MPCQP_ERR_ARG;
+  return mpcqp_set_stance_range(ctx, 0, max_stance);
+}
+
+int mpcqp_set_stance_range(mpcqp_ctx* ctx, int32_t min_stance, int32_t max_stance) {
+  if (!ctx || min_stance < 0 || max_stance < 0 || (max_stance > 0 && min_stance > max_stance)) return MPCQP_ERR_ARG;
+  ctx->stance_min = min_stance;
   ctx->stance_hint = max_stance;
   return MPCQP_OK;
 }
@@ -543,10 +564,15 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   // A robot has n = 3 * #stance <= 12 N variables.  Robots with more than 64 are queued
   // for class 96, more than 96 for class 128, more than 128 for the interior-point
   // class -- each queued launch skipped when no robot can need it (horizon, or the
-  // caller's stance hint).
+  // caller's stance range).  When the range rules out the smaller classes, the first
+  // class that can be needed takes the batch directly (one workgroup per robot) and
+  // routes the larger robots on.
   const int nmax_h = 12 * kp.N;
   const int nmax = ctx->stance_hint > 0 && 3 * ctx->stance_hint < nmax_h ? 3 * ctx->stance_hint : nmax_h;
+  const int nmin = 3 * ctx->stance_min;
   const bool large = nmax > 64, huge = nmax > 96, giant = nmax > 128;
+  // the first class launched: 0 = class 64, 1 = 96, 2 = 128, 3 = interior point
+  const int first = nmin > 128 ? 3 : nmin > 96 ? 2 : nmin > 64 ? 1 : 0;
   int* q = nullptr;
   int cap = 0;
   if (large) {
@@ -558,25 +584,28 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   int* q1 = large ? q : nullptr;
   int* q2 = huge ? q + qstride : nullptr;
   int* q3 = giant ? q + 2 * qstride : nullptr;
-  hipLaunchKernelGGL(mpcqp_kernel_64, dim3(batch), dim3(Cfg<64>::NT), 0, st, kp, (int)batch, x0, xref, contact,
-                     feet, robot, u0, U, (int*)status, (int*)iters, q1, q2, q3);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch: ") + hipGetErrorString(e));
-  if (large) {
+  hipError_t e = hipSuccess;
+  if (first == 0) {
+    hipLaunchKernelGGL(mpcqp_kernel_64, dim3(batch), dim3(Cfg<64>::NT), 0, st, kp, (int)batch, x0, xref, contact,
+                       feet, robot, u0, U, (int*)status, (int*)iters, q1, q2, q3);
+    e = hipGetLastError();
+    if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch: ") + hipGetErrorString(e));
+  }
+  if (large && first <= 1) {
     hipLaunchKernelGGL(mpcqp_kernel_96, dim3(batch), dim3(Cfg<96>::NT), 0, st, kp, x0, xref, contact, feet, robot,
-                       u0, U, (int*)status, (int*)iters, q1, q2);
+                       u0, U, (int*)status, (int*)iters, q1, q2, q3, first == 1 ? (int)batch : 0);
     e = hipGetLastError();
     if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (96): ") + hipGetErrorString(e));
   }
-  if (huge) {
+  if (huge && first <= 2) {
     hipLaunchKernelGGL(mpcqp_kernel_128, dim3(batch), dim3(Cfg<128>::NT), 0, st, kp, x0, xref, contact, feet, robot,
-                       u0, U, (int*)status, (int*)iters, q2);
+                       u0, U, (int*)status, (int*)iters, q2, q3, first == 2 ? (int)batch : 0);
     e = hipGetLastError();
     if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (128): ") + hipGetErrorString(e));
   }
   if (giant) {
     hipLaunchKernelGGL(mpcqp_kernel_ipm, dim3(batch), dim3(LANES), 0, st, kp, x0, xref, contact, feet, robot, u0, U,
-                       (int*)status, (int*)iters, q3);
+                       (int*)status, (int*)iters, q3, first == 3 ? (int)batch : 0);
     e = hipGetLastError();
     if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (ipm): ") + hipGetErrorString(e));
   }

@@ -268,8 +268,8 @@ class ModelPredictiveController():
         copy (and one synchronisation) for U and the status."""
         e = self._engine
         dv = self._dev
-        # the exact stance count of this table: only the capacity classes it needs launch
-        e.set_stance_hint(stance)
+        # the exact stance count of this table: only the capacity class it needs launches
+        e.set_stance_range(stance, stance)
         e.solve_raw(1, dv["x0"], dv["xref"] if xref is None else xref, contact, feet, dv["robot"], dv["u0"],
                     dv["U"], dv["status"], dv["iters"])
         out = dv["out"].cpu().numpy()

@@ -26,6 +26,7 @@ EXPORTED_SYMBOLS = (
     "mpcqp_create",
     "mpcqp_solve",
     "mpcqp_set_stance_hint",
+    "mpcqp_set_stance_range",
     "mpcqp_destroy",
     "mpcqp_last_error",
     "mpcqp_plan",
@@ -33,7 +34,7 @@ EXPORTED_SYMBOLS = (
     "mpcqp_set_planner",
     "mpcqp_stance_torques",
 )
-ABI_VERSION = 2
+ABI_VERSION = 3
 PLAN_STRIDE = 8     # MPCQP_PLAN_STRIDE: float64 planner state per robot
 GAIT_STRIDE = 9     # MPCQP_GAIT_STRIDE: period, offsets[4], durations[4]
 PLAN_REFERENCE = 1      # MPCQP_PLAN_REFERENCE: build X_ref (+ gait table) this tick
@@ -78,6 +79,8 @@ def load():
     lib.mpcqp_solve.argtypes = [vp, i32, f32p, f32p, f32p, f32p, f32p, f32p, f32p, i32p, i32p, vp]
     lib.mpcqp_set_stance_hint.restype = ctypes.c_int
     lib.mpcqp_set_stance_hint.argtypes = [vp, i32]
+    lib.mpcqp_set_stance_range.restype = ctypes.c_int
+    lib.mpcqp_set_stance_range.argtypes = [vp, i32, i32]
     lib.mpcqp_destroy.restype = ctypes.c_int
     lib.mpcqp_destroy.argtypes = [vp]
     lib.mpcqp_last_error.restype = ctypes.c_char_p

@@ -78,7 +78,7 @@ class LinearMpc:
         _lib.check(None, self.lib.mpcqp_create(ctypes.byref(p), int(idx), ctypes.byref(ctx)),
                    "mpcqp_create")
         self._ctx = ctx
-        self._hint = 0
+        self._hint = (0, 0)
         if max_stance:
             self.set_stance_hint(max_stance)
         self.default_robot = self._robot_record(robot)
@@ -87,9 +87,16 @@ class LinearMpc:
         """Promise at most ``max_stance`` stance foot-steps per robot in the following
         solves (0 = no promise): capacity classes above 3 * max_stance variables are
         not launched.  A robot breaking the promise gets MPCQP_STATUS_TOO_LARGE."""
-        if int(max_stance) != getattr(self, "_hint", None):
-            _lib.check(self._ctx, self.lib.mpcqp_set_stance_hint(self._ctx, int(max_stance)), "set_stance_hint")
-            self._hint = int(max_stance)
+        self.set_stance_range(0, max_stance)
+
+    def set_stance_range(self, min_stance, max_stance):
+        """Promise between ``min_stance`` and ``max_stance`` stance foot-steps per robot
+        (include/mpcqp.h): only the capacity classes the range can need are launched,
+        the first of them directly on the batch (the drop-in passes the exact count)."""
+        rng = (int(min_stance), int(max_stance))
+        if rng != getattr(self, "_hint", None):
+            _lib.check(self._ctx, self.lib.mpcqp_set_stance_range(self._ctx, *rng), "set_stance_range")
+            self._hint = rng
 
     def __del__(self):
         ctx = getattr(self, "_ctx", None)

@@ -261,3 +261,36 @@ def test_random_contact_patterns_every_class(N):
         assert rel_err_u0(U[b], x) < TOL_U0, (b, int(stance[b]))
     assert np.all(U[1] == 0) and np.all(u0[1] == 0)
     assert bt["robot"][:, R_NX:R_NZ + 1].shape == (B, 3)
+
+
+def test_stance_range_direct_classes():
+    """mpcqp_set_stance_range: when the range rules out the smaller classes, the first
+    possible class takes the batch directly -- the same kernels and arithmetic as the
+    routed path (bitwise), and robots below the range are still solved (by a larger
+    class) to the oracle's tolerance."""
+    from mpcqp.synthetic import make_batch
+    N = 16
+    bt = make_batch(12, N, seed=21, gaits=("trot10",), robots=("a1", "aliengo"))   # 32 stance steps: class 96
+    bt["contact"][::4] = 1.0                                                      # 64: interior point
+    eng = _engine(N)
+    ref = _solve(eng, bt)
+    eng.set_stance_range(32, 64)   # class 96 direct, the interior-point class queued
+    got = _solve(eng, bt)
+    for x, y in zip(ref, got):
+        np.testing.assert_array_equal(x, y)
+    stand = {k: v[::4].copy() for k, v in bt.items()}
+    eng.set_stance_range(0, 0)
+    ref_s = _solve(eng, stand)
+    eng.set_stance_range(64, 64)   # the interior-point class direct
+    got_s = _solve(eng, stand)
+    for x, y in zip(ref_s, got_s):
+        np.testing.assert_array_equal(x, y)
+    # robots below the range's minimum: N = 10 trot (20 stance steps) through class 96 direct
+    bt10 = make_batch(6, 10, seed=22, gaits=("trot10",), robots=("a1",))
+    eng10 = _engine(10)
+    eng10.set_stance_range(25, 40)
+    u0, U, status, _ = _solve(eng10, bt10)
+    assert (status == 0).all(), status
+    for b in range(6):
+        x, _, _ = oracle_solution(bt10, b, 10)
+        assert rel_err_u0(u0[b], x[:12]) < TOL_U0 and rel_err_u0(U[b], x) < TOL_U0, b
