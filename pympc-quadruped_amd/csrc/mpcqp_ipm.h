@@ -53,11 +53,8 @@ struct alignas(16) IpmShared {
   RobotMeta mt;
   alignas(16) double Bm[12][12];   // B_d rows 0..11 (row 12 is 0)
   alignas(16) double BmT[12][12];  // its transpose
-  union {
-    alignas(16) double CW[12][12];   // factor scratch: B blockdiag(W) (dead once E is formed)
-    alignas(16) double TT[12][12];   // factor scratch: (I + P E)^T, then S_k^T
-  };
-  alignas(16) double E[12][12];    // factor scratch: E_k, then S_k A
+  alignas(16) double TT[12][12];   // factor scratch: (I + P E)^T, then S_k^T
+  alignas(16) double M[kMaxN][144];   // M_k = A^T (I - S_k E_k): lsolve's stage maps (row-major)
   double nmr[3][3];                // h R_z^T: A_d[r][6 + c] (r < 3)
   double x0[16];
   double xr[kMaxN][NX];            // xref, float64
@@ -73,10 +70,11 @@ struct alignas(16) IpmShared {
   alignas(16) double By[kMaxN][NU];
   alignas(16) double Us[kMaxN][NU];   // the IPM iterate while a polish overwrites U
   alignas(16) double X[kMaxN + 1][16];
-  alignas(16) double nu[2][16];
-  alignas(16) double pv[2][16];
-  alignas(16) double dx[2][16];
-  alignas(16) double w[16];
+  alignas(16) double BU[kMaxN][NU];   // gradient: B_d U_k
+  alignas(16) double nuh[kMaxN][NU];  // gradient: adjoint nu_k (rows 0..11)
+  alignas(16) double la[kMaxN][NU], lb[kMaxN][NU], lc[kMaxN][NU];   // lsolve: per-stage vectors
+  alignas(16) double ph[kMaxN][NU];   // lsolve: p_{k+1}, the backward recursion's input at stage k
+  alignas(16) double dxh[kMaxN][NU];  // lsolve: dx_k
   // per stance foot-step interior-point state (row slots 0..5)
   double fs[IPM_NF][6], fl[IPM_NF][6], frp[IPM_NF][6], frd[IPM_NF][4];
   union {
@@ -89,20 +87,11 @@ struct alignas(16) IpmShared {
   int fprev[IPM_NF];               // polish: the rows of the previous try
 };
 
-// 12 / 16 consecutive doubles of a 16-B aligned LDS vector, 16 B per read
+// 12 consecutive doubles of a 16-B aligned LDS vector, 16 B per read
 __device__ __forceinline__ void ld12(double (&v)[12], const double* p) {
   const d2* q = reinterpret_cast<const d2*>(p);
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    const d2 x = q[i];
-    v[2 * i] = x[0];
-    v[2 * i + 1] = x[1];
-  }
-}
-__device__ __forceinline__ void ld16(double (&v)[16], const double* p) {
-  const d2* q = reinterpret_cast<const d2*>(p);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
     const d2 x = q[i];
     v[2 * i] = x[0];
     v[2 * i + 1] = x[1];
@@ -232,114 +221,180 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
 #define IPM_T0() do {} while (0)
 #define IPM_T1(i) do {} while (0)
 #endif
-  // ------------------------------------------------ stage recursions (one wave; LDS
-  // phases separated by fsync).  Nm = A_d - I on the 13-state: rows 0..2 <- h R_z^T
-  // x[6..8]; rows 3..5 <- h x[9..11] (+ h^2/2 x[12] on row 5); row 11 <- h x[12].
+  // ------------------------------------------------ stage recursions (one wave).  Nm =
+  // A_d - I on the 13-state: rows 0..2 <- h R_z^T x[6..8]; rows 3..5 <- h x[9..11]
+  // (+ h^2/2 x[12] on row 5); row 11 <- h x[12].  Every recursion over the stages runs in
+  // registers, lane i holding entry i of the stage vector; its only cross-lane traffic is
+  // readlane of the entries the stage map mixes in.  Everything that does not depend on
+  // the recursion (B_d U_k, the stage gradients, the per-stage matvecs of lsolve) is
+  // computed for all N stages at once in LDS phases: N x 12 entries over the 64 lanes,
+  // operands loaded as whole 12-vectors (6 x 16-B LDS reads issued back to back).
+  //
+  // Lane coefficients of Nm (lane = state row i): (Nm x)_i = sum_s fc[s] x_{6+s}, s = 0..6;
+  // (Nm^T nu)_i = sum_s bc[s] nu_{src(s)}, src = 0, 1, 2, 3, 4, 5, 11.
+  double fc[7], bc[7];
+  {
+    const double h2 = 0.5 * h * h;
+    const int r3 = lane < 3 ? lane : 0, c3 = (lane >= 6 && lane < 9) ? lane - 6 : 0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      fc[c] = lane < 3 ? sm.nmr[r3][c] : 0.0;
+      bc[c] = (lane >= 6 && lane < 9) ? sm.nmr[c][c3] : 0.0;
+    }
+#pragma unroll
+    for (int s = 3; s < 6; ++s) {
+      fc[s] = lane == s ? h : 0.0;       // rows 3..5 <- h x_{row + 6}
+      bc[s] = lane == s + 6 ? h : 0.0;   // rows 9..11 <- h nu_{row - 6}
+    }
+    fc[6] = lane == 5 ? h2 : (lane == 11 ? h : 0.0);
+    bc[5] = lane == 11 ? h : (lane == 12 ? h2 : 0.0);
+    bc[6] = lane == 12 ? h : 0.0;
+  }
+  auto mix7 = [](const double (&cf)[7], const double (&s)[7], double add) -> double {
+    const double a0 = fma(cf[0], s[0], cf[1] * s[1]);
+    const double a1 = fma(cf[2], s[2], cf[3] * s[3]);
+    const double a2 = fma(cf[4], s[4], cf[5] * s[5]);
+    const double a3 = fma(cf[6], s[6], add);
+    return (a0 + a1) + (a2 + a3);
+  };
+
   // sm.gr = H U + g on stance coordinates: forward simulation + adjoint recursion
-  // Every stage phase loads its operands as whole 12-vectors (6 x 16-B LDS reads issued
-  // back to back) and keeps the lane's own rows of B_d in registers: one LDS round trip
-  // per phase instead of one per product term.
   auto gradient = [&]() {
     IPM_T0();
-    double brow[12], bcol[12];   // row `lane` of B_d (lanes < 12); column lane - 32 (lanes 32..43)
-    if (lane < 12) ld12(brow, sm.Bm[lane]);
-    if (lane >= 32 && lane < 44) ld12(bcol, sm.BmT[lane - 32]);
-    if (lane < NX) sm.X[0][lane] = sm.x0[lane];
+    for (int e = lane; e < N * NU; e += NT) {   // B_d U_k, every stage
+      const int k = e / NU, i = e % NU;
+      double bi[12], u[12];
+      ld12(bi, sm.Bm[i]);
+      ld12(u, sm.U[k]);
+      sm.BU[k][i] = dot12(bi, u);
+    }
     fsync<NT>();
+    // x_{k+1} = x_k + Nm x_k + B_d u_k (lane 12, the gravity state, stays constant)
+    double x = lane < NX ? sm.x0[lane] : 0.0;
+    if (lane < NX) sm.X[0][lane] = x;
     for (int k = 0; k < N; ++k) {
-      if (lane < NX) {
-        double x[16], u[12];
-        ld16(x, sm.X[k]);
-        ld12(u, sm.U[k]);
-        double v = x[lane];
-        if (lane < 3) v += sm.nmr[lane][0] * x[6] + sm.nmr[lane][1] * x[7] + sm.nmr[lane][2] * x[8];
-        else if (lane < 6) v += h * x[lane + 6] + (lane == 5 ? 0.5 * h * h * x[12] : 0.0);
-        else if (lane == 11) v += h * x[12];
-        if (lane < 12) v += dot12(brow, u);
-        sm.X[k + 1][lane] = v;
-      }
-      fsync<NT>();
-    }
-    // phase k: lanes 0..12 form nu_k from nu_{k+1}; lanes 32..43 the gradient of stage k + 1
-    for (int k = N - 1; k >= -1; --k) {
-      double np[16];
-      ld16(np, sm.nu[(k + 1) & 1]);
-      if (k >= 0 && lane < NX) {
-        double v = sm.qh[lane] * (sm.X[k + 1][lane] - sm.xr[k][lane]);
-        if (k < N - 1) {
-          double a = np[lane & 15];
-          if (lane >= 6 && lane < 9) a += sm.nmr[0][lane - 6] * np[0] + sm.nmr[1][lane - 6] * np[1] + sm.nmr[2][lane - 6] * np[2];
-          else if (lane >= 9 && lane < 12) a += h * np[(lane - 6) & 15];
-          else if (lane == 12) a += 0.5 * h * h * np[5] + h * np[11];
-          v += a;
-        }
-        sm.nu[k & 1][lane] = v;
-      }
-      if (k + 1 < N && lane >= 32 && lane < 32 + NU) {
-        const int c = lane - 32, kk = k + 1;
-        const bool st = sm.mt.stance_of[4 * kk + c / 3] >= 0;
-        double nv[12];
+      const double bu = sm.BU[k][lane < NU ? lane : 0];
+      double s[7];
 #pragma unroll
-        for (int i = 0; i < 12; ++i) nv[i] = np[i];
-        const double g = sm.rh[c] * sm.U[kk][c] + dot12(bcol, nv);
-        sm.gr[kk][c] = st ? g : 0.0;
-      }
-      fsync<NT>();
+      for (int t = 0; t < 7; ++t) s[t] = readlane_d(x, 6 + t);
+      x += mix7(fc, s, lane < NU ? bu : 0.0);
+      if (lane < NX) sm.X[k + 1][lane] = x;   // read back by the same lane below
     }
+    // nu_k = Qh (x_{k+1} - xref_k) + (I + Nm^T) nu_{k+1}
+    double nu = 0.0;
+    const int li = lane < NX ? lane : 0;
+    for (int k = N - 1; k >= 0; --k) {
+      double v = lane < NX ? sm.qh[li] * (sm.X[k + 1][li] - sm.xr[k][li]) : 0.0;
+      if (k < N - 1) {
+        double s[7];
+#pragma unroll
+        for (int t = 0; t < 6; ++t) s[t] = readlane_d(nu, t);
+        s[6] = readlane_d(nu, 11);
+        v += nu + mix7(bc, s, 0.0);
+      }
+      nu = v;
+      if (lane < NU) sm.nuh[k][lane] = nu;
+    }
+    fsync<NT>();
+    for (int e = lane; e < N * NU; e += NT) {   // stage gradients R u_k + B_d^T nu_k
+      const int k = e / NU, c = e % NU;
+      double bcl[12], nv[12];
+      ld12(bcl, sm.BmT[c]);
+      ld12(nv, sm.nuh[k]);
+      const double g = sm.rh[c] * sm.U[k][c] + dot12(bcl, nv);
+      sm.gr[k][c] = sm.mt.stance_of[4 * k + c / 3] >= 0 ? g : 0.0;
+    }
+    fsync<NT>();
     IPM_T1(0);
   };
 
-  // Riccati factorisation with the per-foot-step weights sm.W: S_k for every stage.
-  // Per stage (P = P_{k+1} symmetric): CW = B blockdiag(W) (entry (m, c) = W_leg(c) row .
-  // B[m][leg(c)]), E = B CW^T (symmetric), T^T = (I + P E)^T; lane j < 12 holds column j
-  // of T and lane 12 + j column j of P in registers for the Gauss-Jordan sweep on [T | P]
-  // (pivot column broadcast by readlane); S_k = T^-1 P symmetrised; P_k = Qh + A^T S_k A.
+  // Riccati factorisation with the per-foot-step weights sm.W: S_k and M_k for every
+  // stage, the 12 x 12 stage products on the f64 matrix cores.  v_mfma_f64_16x16x4f64
+  // (tools/ubench/mfma_f64_check.hip; lr = lane >> 4, lc = lane & 15): the A operand of
+  // K-chunk q is A[lc][4q + lr], the B operand B[4q + lr][lc], result register i
+  // D[lr + 4i][lc] -- so result register q of a matrix IS its B operand of chunk q, and
+  // its A operand when the matrix is symmetric; the recursion P -> T -> S -> P stays in
+  // registers (12 x 12 padded to 16 x 16) except for the Gauss-Jordan sweep.  Per stage:
+  //   E = B_d blockdiag(W_k) B_d^T   (blockdiag(W_k) B_d^T formed on the VALU in B-operand form)
+  //   T = I + P E;  S = T^-1 P by Gauss-Jordan on [T | P] (lane j < 12 holds column j of T,
+  //       lane 12 + j column j of P; pivot column by readlane), symmetrised
+  //   P <- Qh + A^T S A;  M_k = A^T (I - S E)     (A = I + Nm; Nm has rows 0..5 only, so
+  //       a product with Nm or Nm^T is 2 K-chunks)
+  // (information form; the textbook P - P B (R + B^T P B)^-1 B^T P loses ~4 digits here).
+  // The critical path per stage is S -> P -> T -> sweep; E of the next stage and M of the
+  // previous one are issued before the sweep, so the matrix cores run them under it.
+  const int lr = lane >> 4, lc = lane & 15;
+  const int lcc = lc < 12 ? lc : 0;
+  double Nmb[2], Bop[3], bx[3][3];   // Nm[4q+lr][lc]; B_d[lc][4q+lr]; B_d[lc][3 leg(4q+lr) + a]
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int c = 4 * q + lr;
+    const bool ok = c < 12 && lc < 12;
+    const int cc = ok ? c : 0;
+    if (q < 2) {
+      double nv = 0.0;
+      if (c < 3 && lc >= 6 && lc < 9) nv = sm.nmr[cc][lc - 6];
+      else if (c >= 3 && c < 6 && lc == c + 6) nv = h;
+      Nmb[q] = nv;
+    }
+    Bop[q] = ok ? sm.Bm[lcc][cc] : 0.0;
+#pragma unroll
+    for (int a2 = 0; a2 < 3; ++a2) bx[q][a2] = ok ? sm.Bm[lcc][3 * (cc / 3) + a2] : 0.0;
+  }
+  auto diag4 = [&](double d) -> d4 {   // d I (12 x 12) in result layout
+    d4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = (lr + 4 * i == lc && lc < 12) ? d : 0.0;
+    return v;
+  };
+  auto mfma = [](double a, double b, d4 c) -> d4 { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); };
+  auto stage_e = [&](int k) -> d4 {   // E_k
+    d4 Er = diag4(0.0);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int c = 4 * q + lr;
+      double x = 0.0;
+      if (c < 12 && lc < 12) {
+        const int j = sm.mt.stance_of[4 * k + c / 3];
+        if (j >= 0) {
+          const double* w = sm.W[j] + 3 * (c % 3);
+          x = w[0] * bx[q][0] + w[1] * bx[q][1] + w[2] * bx[q][2];
+        }
+      }
+      Er = mfma(Bop[q], x, Er);
+    }
+    return Er;
+  };
+  auto stage_m = [&](int k, const d4& Sr, const d4& Er) {   // M_k = (I + Nm^T) (I - S E) -> sm.M[k]
+    d4 Lr = diag4(1.0);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) Lr = mfma(-Sr[q], Er[q], Lr);
+    d4 Mr = Lr;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) Mr = mfma(Nmb[q], Lr[q], Mr);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = lr + 4 * i;
+      if (r < 12 && lc < 12) sm.M[k][12 * r + lc] = Mr[i];
+    }
+  };
+
   auto factor = [&]() {
     IPM_T0();
-    for (int e = lane; e < 144; e += NT) sm.P[e] = (e / 12 == e % 12) ? sm.qh[e / 12] : 0.0;
-    fsync<NT>();
+    d4 Pr = diag4(sm.qh[lcc]);
+    d4 Er = stage_e(N - 1), Sp = diag4(0.0), Ep = diag4(0.0);
     const int jc = lane < 12 ? lane : (lane < 24 ? lane - 12 : 0);
     for (int k = N - 1; k >= 0; --k) {
       IPM_TS(ta);
-      // CW[m][c] (zero columns for swing legs)
+      d4 Tr = diag4(1.0);
 #pragma unroll
-      for (int t = 0; t < 3; ++t) {
-        const int e = lane + NT * t;
-        if (e < 144) {
-          const int m = e / 12, c = e % 12, l = c / 3, a = c % 3;
-          const int j = sm.mt.stance_of[4 * k + l];
-          double v = 0.0;
-          if (j >= 0) {
-            const double* wr = sm.W[j] + 3 * a;
-            v = wr[0] * sm.Bm[m][3 * l] + wr[1] * sm.Bm[m][3 * l + 1] + wr[2] * sm.Bm[m][3 * l + 2];
-          }
-          sm.CW[m][c] = v;
-        }
-      }
-      fsync<NT>();
-      // E[i][m] = B row i . CW row m
+      for (int q = 0; q < 3; ++q) Tr = mfma(Pr[q], Er[q], Tr);
 #pragma unroll
-      for (int t = 0; t < 3; ++t) {
-        const int e = lane + NT * t;
-        if (e < 144) {
-          const int i = e / 12, m = e % 12;
-          double bi[12], cm[12];
-          ld12(bi, sm.Bm[i]);
-          ld12(cm, sm.CW[m]);
-          sm.E[i][m] = dot12(bi, cm);
-        }
-      }
-      fsync<NT>();
-      // T[i][j] = delta + P row i . E row j (E symmetric), stored transposed
-#pragma unroll
-      for (int t = 0; t < 3; ++t) {
-        const int e = lane + NT * t;
-        if (e < 144) {
-          const int i = e / 12, j = e % 12;
-          double pi[12], ej[12];
-          ld12(pi, sm.P + 12 * i);
-          ld12(ej, sm.E[j]);
-          sm.TT[j][i] = dot12(pi, ej) + (i == j ? 1.0 : 0.0);
+      for (int i = 0; i < 4; ++i) {
+        const int r = lr + 4 * i;
+        if (r < 12 && lc < 12) {
+          sm.TT[lc][r] = Tr[i];
+          sm.P[12 * r + lc] = Pr[i];
         }
       }
       fsync<NT>();
@@ -347,6 +402,9 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       double col[12];
       if (lane < 12) ld12(col, sm.TT[jc]);
       else ld12(col, sm.P + 12 * jc);   // column jc of P = row jc (P symmetric)
+      // under the sweep: M of the previous stage, E of the next
+      if (k < N - 1) stage_m(k + 1, Sp, Ep);
+      const d4 En = k > 0 ? stage_e(k - 1) : diag4(0.0);
 #pragma unroll
       for (int kk = 0; kk < 12; ++kk) {
         double pc[12];
@@ -364,144 +422,176 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       IPM_TA(4, ta, tb);
       IPM_TA(5, tb, tc);
       IPM_TA(6, tc, td);
-      // S_k = (S + S^T) / 2 (sm.TT holds S^T); S_k A into sm.E
+      d4 Sr;   // S_k = (S + S^T) / 2, kept for lsolve
 #pragma unroll
-      for (int t = 0; t < 3; ++t) {
-        const int e = lane + NT * t;
-        if (e < 144) {
-          const int i = e / 12, j = e % 12;
-          auto ss = [&](int m, int n) -> double { return 0.5 * (sm.TT[m][n] + sm.TT[n][m]); };
-          double v = ss(i, j);
-          sm.S[k][e] = v;
-          if (j >= 6 && j < 9) v += ss(i, 0) * sm.nmr[0][j - 6] + ss(i, 1) * sm.nmr[1][j - 6] + ss(i, 2) * sm.nmr[2][j - 6];
-          else if (j >= 9) v += h * ss(i, j - 6);
-          sm.E[i][j] = v;
+      for (int i = 0; i < 4; ++i) {
+        const int r = lr + 4 * i;
+        double v = 0.0;
+        if (r < 12 && lc < 12) {
+          v = 0.5 * (sm.TT[lc][r] + sm.TT[r][lc]);
+          sm.S[k][12 * r + lc] = v;
         }
+        Sr[i] = v;
       }
-      fsync<NT>();
+      if (k > 0) {   // P_k = Qh + (I + Nm^T) S (I + Nm)
+        d4 SA = Sr;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) SA = mfma(Sr[q], Nmb[q], SA);
+        Pr = diag4(sm.qh[lcc]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Pr[i] += SA[i];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) Pr = mfma(Nmb[q], SA[q], Pr);
+      }
+      Sp = Sr;
+      Ep = Er;
+      Er = En;
       IPM_TS(te);
       IPM_TA(7, td, te);
-      if (k > 0) {   // P_k = Qh + A^T (S_k A)
-#pragma unroll
-        for (int t = 0; t < 3; ++t) {
-          const int e = lane + NT * t;
-          if (e < 144) {
-            const int i = e / 12, j = e % 12;
-            double v = sm.E[i][j];
-            if (i >= 6 && i < 9) v += sm.nmr[0][i - 6] * sm.E[0][j] + sm.nmr[1][i - 6] * sm.E[1][j] + sm.nmr[2][i - 6] * sm.E[2][j];
-            else if (i >= 9) v += h * sm.E[i - 6][j];
-            if (i == j) v += sm.qh[i];
-            sm.P[e] = v;
-          }
-        }
-        fsync<NT>();
-      }
     }
+    stage_m(0, Sp, Ep);
+    fsync<NT>();   // S_k, M_k for lsolve
     IPM_T1(1);
   };
 
   // (H + G^T D G) d = rhs restricted to the foot-steps' subspaces: sm.rhs -> sm.dU
+  // The Riccati sweep in affine form (factor's M_k = A^T (I - S_k E_k), E_k = B W_k B^T):
+  //   backward  Y_k = W_k (B^T p_{k+1} - rhs_k),  p_k = A^T (p_{k+1} - S_k B Y_k)
+  //                                              = M_k p_{k+1} + A^T S_k B W_k rhs_k,
+  //   forward   d_k = W_k B^T S_k (B Y_k - A dx_k) - Y_k,  dx_{k+1} = A dx_k + B d_k
+  //                                              = M_k^T dx_k + B (W_k B^T S_k B Y_k - Y_k),
+  // so each recursion is one 12 x 12 matvec per stage (12 lanes, readlane of the vector)
+  // and every other product runs for all stages at once.
+  // W_k B^T x restricted to entry c (leg l = c / 3): the leg's 3 x 3 weight row times the
+  // leg's three B_d columns against x; 0 for a swing leg
+  auto wbt = [&](int k, int c, const double (&x)[12], const double (*sub)) -> double {
+    const int l = c / 3, a = c % 3;
+    const int j = sm.mt.stance_of[4 * k + l];
+    if (j < 0) return 0.0;
+    double b0[12], b1[12], b2[12];
+    ld12(b0, sm.BmT[3 * l]);
+    ld12(b1, sm.BmT[3 * l + 1]);
+    ld12(b2, sm.BmT[3 * l + 2]);
+    const double z0 = dot12(b0, x) - (sub ? sub[3 * l] : 0.0);
+    const double z1 = dot12(b1, x) - (sub ? sub[3 * l + 1] : 0.0);
+    const double z2 = dot12(b2, x) - (sub ? sub[3 * l + 2] : 0.0);
+    const double* wj = sm.W[j] + 3 * a;
+    return wj[0] * z0 + wj[1] * z1 + wj[2] * z2;
+  };
+  auto bmat = [&](double (*dst)[NU], double (*src)[NU]) {   // dst_k = B_d src_k, every stage
+    for (int e = lane; e < N * NU; e += NT) {
+      const int k = e / NU, i = e % NU;
+      double bi[12], v[12];
+      ld12(bi, sm.Bm[i]);
+      ld12(v, src[k]);
+      dst[k][i] = dot12(bi, v);
+    }
+    fsync<NT>();
+  };
+  auto smat = [&](double (*dst)[NU], double (*src)[NU]) {   // dst_k = S_k src_k, every stage
+    for (int e = lane; e < N * NU; e += NT) {
+      const int k = e / NU, i = e % NU;
+      double sr[12], v[12];
+      ld12(sr, sm.S[k] + 12 * i);
+      ld12(v, src[k]);
+      dst[k][i] = dot12(sr, v);
+    }
+    fsync<NT>();
+  };
+  const int l12 = lane < NU ? lane : 0;
+
   auto lsolve = [&]() {
     IPM_T0();
-    // lanes c < 12: the three B_d columns of the lane's leg and B_d row c
-    double bl0[12], bl1[12], bl2[12], brow[12];
-    if (lane < 12) {
-      const int l = lane / 3;
-      ld12(bl0, sm.BmT[3 * l]);
-      ld12(bl1, sm.BmT[3 * l + 1]);
-      ld12(bl2, sm.BmT[3 * l + 2]);
-      ld12(brow, sm.Bm[lane]);
+    for (int e = lane; e < N * NU; e += NT) {   // la_k = W_k rhs_k
+      const int k = e / NU, c = e % NU, l = c / 3, a = c % 3;
+      const int j = sm.mt.stance_of[4 * k + l];
+      double v = 0.0;
+      if (j >= 0) {
+        const double* wj = sm.W[j] + 3 * a;
+        v = wj[0] * sm.rhs[k][3 * l] + wj[1] * sm.rhs[k][3 * l + 1] + wj[2] * sm.rhs[k][3 * l + 2];
+      }
+      sm.la[k][c] = v;
     }
-    if (lane < 16) sm.pv[0][lane] = 0.0;
     fsync<NT>();
-    int pb = 0;
+    bmat(sm.lb, sm.la);   // B W rhs
+    smat(sm.la, sm.lb);   // S B W rhs
+    for (int e = lane; e < N * NU; e += NT) {   // lc_k = A^T la_k
+      const int k = e / NU, i = e % NU;
+      double v = sm.la[k][i];
+      if (i >= 6 && i < 9) v += sm.nmr[0][i - 6] * sm.la[k][0] + sm.nmr[1][i - 6] * sm.la[k][1] + sm.nmr[2][i - 6] * sm.la[k][2];
+      else if (i >= 9) v += h * sm.la[k][i - 6];
+      sm.lc[k][i] = v;
+    }
+    fsync<NT>();
+    // backward recursion: lane i < 12 holds p_i
+    double p = 0.0;
     for (int k = N - 1; k >= 0; --k) {
-      if (lane < NU) {   // Y = W (B_leg^T p - rhs_leg) for the lane's leg
-        const int l = lane / 3, a = lane % 3;
-        const int j = sm.mt.stance_of[4 * k + l];
-        double y = 0.0;
-        if (j >= 0) {
-          double p[12];
-          ld12(p, sm.pv[pb]);
-          const double z0 = dot12(bl0, p) - sm.rhs[k][3 * l];
-          const double z1 = dot12(bl1, p) - sm.rhs[k][3 * l + 1];
-          const double z2 = dot12(bl2, p) - sm.rhs[k][3 * l + 2];
-          const double* wj = sm.W[j] + 3 * a;
-          y = wj[0] * z0 + wj[1] * z1 + wj[2] * z2;
-        }
-        sm.Y[k][lane] = y;
-      }
-      fsync<NT>();
-      if (lane < 12) {
-        double y[12];
-        ld12(y, sm.Y[k]);
-        sm.By[k][lane] = dot12(brow, y);
-      }
-      fsync<NT>();
-      if (k > 0) {   // p <- A^T (p - S_k By)
-        if (lane < 12) {
-          double by[12], sr[12];
-          ld12(by, sm.By[k]);
-          const double* p = sm.pv[pb];
-          auto tt = [&](int m) -> double {
-            ld12(sr, sm.S[k] + 12 * m);
-            return p[m] - dot12(sr, by);
-          };
-          double v = tt(lane);
-          if (lane >= 6 && lane < 9) v += sm.nmr[0][lane - 6] * tt(0) + sm.nmr[1][lane - 6] * tt(1) + sm.nmr[2][lane - 6] * tt(2);
-          else if (lane >= 9) v += h * tt(lane - 6);
-          sm.pv[pb ^ 1][lane] = v;
-        }
-        pb ^= 1;
-        fsync<NT>();
+      if (lane < NU) sm.ph[k][lane] = p;
+      if (k > 0) {
+        double mr[12], r[12];
+        ld12(mr, sm.M[k] + 12 * l12);
+        const double ck = sm.lc[k][l12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) r[j] = readlane_d(p, j);
+        p = lane < NU ? dot12(mr, r) + ck : 0.0;
       }
     }
-    if (lane < 16) sm.dx[0][lane] = 0.0;
     fsync<NT>();
-    int db = 0;
-    for (int k = 0; k < N; ++k) {
-      double dxv[12], adx[12];
-      ld12(dxv, sm.dx[db]);
-#pragma unroll
-      for (int i = 0; i < 12; ++i) {   // A dx on the 12-state
-        double a = dxv[i];
-        if (i < 3) a += sm.nmr[i][0] * dxv[6] + sm.nmr[i][1] * dxv[7] + sm.nmr[i][2] * dxv[8];
-        else if (i < 6) a += h * dxv[i + 6];
-        adx[i] = a;
-      }
-      if (lane < 12) {   // w = S_k (By - A dx)
-        double sr[12], by[12];
-        ld12(sr, sm.S[k] + 12 * lane);
-        ld12(by, sm.By[k]);
-#pragma unroll
-        for (int m = 0; m < 12; ++m) by[m] -= adx[m];
-        sm.w[lane] = dot12(sr, by);
-      }
-      fsync<NT>();
-      if (lane < NU) {   // d = W B_leg^T w - Y
-        const int l = lane / 3, a = lane % 3;
-        const int j = sm.mt.stance_of[4 * k + l];
-        double d = 0.0;
-        if (j >= 0) {
-          double w[12];
-          ld12(w, sm.w);
-          const double* wj = sm.W[j] + 3 * a;
-          d = wj[0] * dot12(bl0, w) + wj[1] * dot12(bl1, w) + wj[2] * dot12(bl2, w) - sm.Y[k][lane];
-        }
-        sm.dU[k][lane] = d;
-      }
-      fsync<NT>();
-      if (lane < 12) {   // dx <- A dx + B d
-        double du[12];
-        ld12(du, sm.dU[k]);
-        double a = adx[0];
-#pragma unroll
-        for (int i = 1; i < 12; ++i) a = (lane == i) ? adx[i] : a;
-        sm.dx[db ^ 1][lane] = a + dot12(brow, du);
-      }
-      db ^= 1;
-      fsync<NT>();
+    for (int e = lane; e < N * NU; e += NT) {   // Y_k = W_k (B^T p_{k+1} - rhs_k)
+      const int k = e / NU, c = e % NU;
+      double pk[12];
+      ld12(pk, sm.ph[k]);
+      sm.Y[k][c] = wbt(k, c, pk, sm.rhs[k]);
     }
+    fsync<NT>();
+    bmat(sm.By, sm.Y);    // B Y
+    smat(sm.la, sm.By);   // S B Y
+    for (int e = lane; e < N * NU; e += NT) {   // lb_k = W_k B^T S_k B Y_k - Y_k
+      const int k = e / NU, c = e % NU;
+      double sk[12];
+      ld12(sk, sm.la[k]);
+      sm.lb[k][c] = wbt(k, c, sk, nullptr) - sm.Y[k][c];
+    }
+    fsync<NT>();
+    bmat(sm.lc, sm.lb);   // B lb
+    // forward recursion: lane i < 12 holds dx_i; dx_{k+1} = M_k^T dx_k + lc_k
+    double dx = 0.0;
+    for (int k = 0; k < N; ++k) {
+      if (lane < NU) sm.dxh[k][lane] = dx;
+      if (k < N - 1) {
+        double mc[12], r[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) mc[j] = sm.M[k][12 * j + l12];
+        const double ek = sm.lc[k][l12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) r[j] = readlane_d(dx, j);
+        dx = lane < NU ? dot12(mc, r) + ek : 0.0;
+      }
+    }
+    fsync<NT>();
+    for (int e = lane; e < N * NU; e += NT) {   // la_k = S_k (B Y_k - A dx_k)
+      const int k = e / NU, i = e % NU;
+      double dxv[12], by[12], sr[12];
+      ld12(dxv, sm.dxh[k]);
+      ld12(by, sm.By[k]);
+      ld12(sr, sm.S[k] + 12 * i);
+#pragma unroll
+      for (int m = 0; m < 12; ++m) {   // A dx on the 12-state
+        double a = dxv[m];
+        if (m < 3) a += sm.nmr[m][0] * dxv[6] + sm.nmr[m][1] * dxv[7] + sm.nmr[m][2] * dxv[8];
+        else if (m < 6) a += h * dxv[m + 6];
+        by[m] -= a;
+      }
+      sm.la[k][i] = dot12(sr, by);
+    }
+    fsync<NT>();
+    for (int e = lane; e < N * NU; e += NT) {   // d_k = W_k B^T la_k - Y_k
+      const int k = e / NU, c = e % NU;
+      double w[12];
+      ld12(w, sm.la[k]);
+      sm.dU[k][c] = wbt(k, c, w, nullptr) - sm.Y[k][c];
+    }
+    fsync<NT>();
     IPM_T1(2);
   };
 

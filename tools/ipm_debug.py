@@ -10,7 +10,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "pympc-quadruped_amd"), os.path.join(ROOT, "tests")]
-DBG = os.path.join(ROOT, "tools", "libmpcqp_ipmdbg.so")
+DBG = os.environ.get("IPM_DBG_LIB", os.path.join(ROOT, "tools", "libmpcqp_ipmdbg.so"))
 
 if len(sys.argv) > 1 and sys.argv[1] == "build":
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
