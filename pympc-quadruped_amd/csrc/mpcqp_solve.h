@@ -465,18 +465,28 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
   for (int w = 1; w < C::NW; ++w) wscale = fmax(wscale, sm.wmax[w]);
   wscale = sgpr_d(wscale);
+  const float qfloor = fmaxf((float)(1e-9 * wscale), 1e-30f);   // rows dependent on the active set
 
   // ---- per-lane constraint rows c = lane + 64k (redundant in every wave): the
   // row's foot-step variables start at cz, its cone coefficients at sm.mt.rows[crt]
   // (re-read from LDS: registers hold the two tiles); s = a_c . x - b_c.
-  // Row choice: the violated row with the most negative s_c / sqrt(a_c^T W a_c)
-  // (violation in the dual metric), which needs fewer add/drop cycles than the
-  // raw most-violated rule.  With mu > 0 the n.f >= 0 row is implied by the two
-  // opposite t1 rows and never enters (s = +inf): it only adds degenerate steps
-  // at the cone apex.  Neither choice changes the (unique) optimum.
+  // Row choice: the violated row with the most negative s_c / sqrt(a_c^T P a_c), P the
+  // current projected inverse Hessian -- the row whose full step raises the dual
+  // objective most (s_c^2 / (2 a_c^T P a_c)); tools/gi_sim.py: the slowest robot of a
+  // config-2 batch needs 8-17 % fewer passes than with the initial metric W.  q_c =
+  // a_c^T P a_c is kept per row by the rank-1/2 updates of P: an add subtracts
+  // (a_c . z)^2 / (a_p . z) (a_c . z = zs_c is computed for every row anyway), a pair
+  // [zs, zs2] S^-1 [zs, zs2]^T, a drop adds (a_c . R_l)^2 / eta.  q_c is held in f32
+  // (one VGPR per row, as the f32 key it scales): the choice is a heuristic, and any
+  // choice reaches the same optimum.  With mu > 0 the n.f >= 0 row is implied by the
+  // two opposite t1 rows and never enters (s = +inf): it only adds degenerate steps at
+  // the cone apex.
   int cz[CPL], crt[CPL];
   double s[CPL];
-  float rn[CPL];   // 1 / sqrt(a_c^T W a_c): only scales the f32-preselected row key
+  // classes 96 / 128 keep the initial metric: their launches are throughput-bound and
+  // the per-pass updates cost more than the passes they save (configs 4 / 5: -3 / -1 %)
+  constexpr bool kCurKey = NV == 64;
+  float qm[CPL];   // a_c^T P a_c (f32; classes 96 / 128: 1 / sqrt(a_c^T W a_c)): scales the f32 row key
   auto cdot = [&](const double* v, int k) -> double {
     const double* a = sm.mt.rows[crt[k]];
     const double* vf = v + cz[k];
@@ -498,7 +508,8 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     double q = 0.0;
 #pragma unroll
     for (int i = 0; i < 3; ++i) q = fma(a[i], fma(w[3 * i], a[0], fma(w[3 * i + 1], a[1], w[3 * i + 2] * a[2])), q);
-    rn[k] = ok && q > 0.0 ? (float)__builtin_amdgcn_rsq(q) : 1.0f;
+    if constexpr (kCurKey) qm[k] = ok && q > 0.0 ? (float)q : 1.0f;
+    else qm[k] = ok && q > 0.0 ? (float)__builtin_amdgcn_rsq(q) : 1.0f;
   }
   double x[VPL], u[VPL];
 #pragma unroll
@@ -540,7 +551,8 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       // most violated row in the dual metric (f32-rounded keys, lowest lane on ties)
       double key[CPL];
 #pragma unroll
-      for (int k = 0; k < CPL; ++k) key[k] = s[k] < -tol ? s[k] * (double)rn[k] : INFINITY;
+      for (int k = 0; k < CPL; ++k)
+        key[k] = s[k] < -tol ? s[k] * (double)(kCurKey ? __builtin_amdgcn_rsqf(fmaxf(qm[k], qfloor)) : qm[k]) : INFINITY;
       double bv = key[0];
       int bk = 0;
 #pragma unroll
@@ -739,6 +751,10 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         // rank-2 updates: row coefficients (al, be) = S^-1 (row's pair), then
         // M[r][c] -= al cz1[c] + be cz2[c]
         const double i11 = s22 * id, i12 = -s12 * id, i22 = zsp * id;
+        if constexpr (kCurKey)
+#pragma unroll
+          for (int k = 0; k < CPL; ++k)
+            qm[k] = (float)((double)qm[k] - fma(i11 * zs[k], zs[k], fma(2.0 * i12 * zs[k], zs2[k], i22 * zs2[k] * zs2[k])));
         double cz1[TW], cz2[TW], z41[4], z42[4];
         ldt<TW>(cz1, vz, tc);
         ldt<TW>(cz2, vz2, tc);
@@ -813,6 +829,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     // rank-1 updates  W += aW cv^T,  R += aR cv^T  (rows by the lane's tile row)
     double aW[4], aR[4], cv[TW];
     int zrow = -1;   // R row to clear (drop)
+    double iedrop = 0.0;   // 1 / eta of a drop
     if (add) {
       // slot q (first free); P -= z z^T / sigma ; R -= (r - e_q) z^T / sigma
       int q = 0;
@@ -820,6 +837,9 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       for (int k = VPL - 1; k >= 0; --k)
         if (~occ[k]) q = LANES * k + __builtin_ctzll(~occ[k]);
       const double is = rcp_nr(zsp);
+      if constexpr (kCurKey)
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) qm[k] = (float)fma(-zs[k] * zs[k], is, (double)qm[k]);
       double zr4[4], rr4[4];
       ld4(zr4, vz, tr);
       ldt<TW>(cv, vz, tc);
@@ -869,6 +889,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       }
       fsync<NT>();
       const double ie = rcp_nr(sm.yv[l]);
+      iedrop = ie;
       double rl4[4], yv4[4];
       ld4(rl4, sm.rl, tr);
       ld4(yv4, sm.yv, tr);
@@ -895,6 +916,13 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         for (int c = 0; c < TW; ++c) Rm[r][c] = fma(aR[r], cv[c], Rm[r][c]);
     }
     if (zrow >= 0) {
+      if constexpr (kCurKey) {
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {   // q_c += (a_c . R_l)^2 / eta (sm.rl holds R_l until the next drop)
+          const double ar = cdot(sm.rl, k);
+          qm[k] = (float)fma(ar * ar, iedrop, (double)qm[k]);
+        }
+      }
       if (tr == (zrow >> 2)) {   // clear row l of R exactly
         const int lr = zrow & 3;
 #pragma unroll

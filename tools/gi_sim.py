@@ -6,7 +6,7 @@ rows from distinct foot-steps added at once when the equality-constrained step
 keeps every multiplier positive (nested fallback to fewer rows, then a single
 GI step).  Decisions follow the engine: the most violated row in the dual metric
 (scaled by the initial W), partner rows the best of other foot-steps.
-Usage: python tools/gi_sim.py [B] [k ...]
+Usage: python tools/gi_sim.py [B] [k ...]   (GI_METRIC=W: rows keyed in the initial metric)
 """
 import os
 import sys
@@ -53,7 +53,8 @@ def robot_qp(bt, b, N):
     return H, g, np.array(A), np.array(bb), np.array(foot)
 
 
-def simulate(H, g, A, b, foot, kmax, tol=1e-9, max_pass=2000, ratio=0.0, stop_after_drops=10**9, W0=None):
+def simulate(H, g, A, b, foot, kmax, tol=1e-9, max_pass=2000, ratio=0.0, stop_after_drops=10**9, W0=None,
+             metric="P"):
     n = H.shape[0]
     W = np.linalg.inv(H) if W0 is None else W0.copy()
     P = W.copy()
@@ -72,7 +73,11 @@ def simulate(H, g, A, b, foot, kmax, tol=1e-9, max_pass=2000, ratio=0.0, stop_af
         s = A @ x - b
         s[slot_row[occ]] = np.inf        # active rows
         if p < 0:
-            key = np.where(s < -tol, s * rn, np.inf)
+            if metric == "P":   # the kernel's rule: current metric a P a (steepest dual ascent)
+                scale = 1.0 / np.sqrt(np.maximum(np.einsum("ij,jk,ik->i", A, P, A), 1e-9 * wscale))
+            else:               # round-1/2 rule: initial metric a W a
+                scale = rn
+            key = np.where(s < -tol, s * scale, np.inf)
             if not np.isfinite(key.min()):
                 break
             cands = []
@@ -188,7 +193,8 @@ def main():
         parts = ka.split(":")   # "k", "k:ratio" or "k:ratio:drops"
         k, r = int(parts[0]), float(parts[1]) if len(parts) > 1 else 0.0
         sd = int(parts[2]) if len(parts) > 2 else 10**9
-        res = [simulate(*qp, kmax=k, ratio=r, stop_after_drops=sd) for qp in qps]
+        res = [simulate(*qp, kmax=k, ratio=r, stop_after_drops=sd, metric=os.environ.get("GI_METRIC", "P"))
+               for qp in qps]
         passes = np.array([r["passes"] for r in res])
         its = np.array([r["it"] for r in res])
         drops = np.array([r["drops"] for r in res])
