@@ -56,6 +56,8 @@ def parse():
                     help="diagnostics: one HIP event pair per step (perturbs back-to-back dispatch, "
                          "~5%% slower steps); default: one pair around the timed loop")
     ap.add_argument("--no-callers", action="store_true", help="skip the planner/torque kernel timing")
+    ap.add_argument("--event-every", type=int, default=8,
+                    help="N > 1: bracket every k-th step's solve and gather with HIP events (sampled)")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "latest", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -421,8 +423,12 @@ def main():
             step(k)
         events[0][1].record(stream)
     else:
+        # per-step event pairs cost ~6 us a step: bracket a sample of the steps
+        # (every --event-every-th; every step with --step-events)
+        every = 1 if args.step_events else max(1, args.event_every)
         for k in range(args.steps):
-            step(k, events[k])
+            step(k, events[k] if k % every == 0 else None)
+        events = [e for k, e in enumerate(events) if k % every == 0]
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
