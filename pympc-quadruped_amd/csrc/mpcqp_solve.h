@@ -768,14 +768,14 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
           for (int c = 0; c < TW; ++c) W[r][c] = fma(-be, cz2[c], fma(-al, cz1[c], W[r][c]));
         }
         if (rlive || slots_live(RPW * wave)) {
-          double r41[4], r42[4];
-          ld4(r41, vr, tr);
-          ld4(r42, vr2, tr);
+          // r / r2 entries read per row (not as two 4-vectors): the shorter live
+          // ranges keep the kernel spill-free (a 4-byte VGPR spill here otherwise,
+          // written back as ~266 KiB of scratch per config-2 launch)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int sl = 4 * tr + r;
-            const double e1 = r41[r] - (sl == qa ? 1.0 : 0.0);
-            const double e2 = r42[r] - (sl == qb ? 1.0 : 0.0);
+            const double e1 = vr[sl] - (sl == qa ? 1.0 : 0.0);
+            const double e2 = vr2[sl] - (sl == qb ? 1.0 : 0.0);
             const double al = fma(i11, e1, i12 * e2);
             const double be = fma(i12, e1, i22 * e2);
 #pragma unroll

@@ -54,7 +54,7 @@ def robot_qp(bt, b, N):
 
 
 def simulate(H, g, A, b, foot, kmax, tol=1e-9, max_pass=2000, ratio=0.0, stop_after_drops=10**9, W0=None,
-             metric="P"):
+             metric="P", init_rows=None):
     n = H.shape[0]
     W = np.linalg.inv(H) if W0 is None else W0.copy()
     P = W.copy()
@@ -63,6 +63,21 @@ def simulate(H, g, A, b, foot, kmax, tol=1e-9, max_pass=2000, ratio=0.0, stop_af
     slot_row = -np.ones(n, int)
     u = np.zeros(n)
     x = -W @ g
+    if init_rows is not None and len(init_rows):
+        # warm start: the equality-constrained optimum on init_rows (a valid dual
+        # active-set iterate when every multiplier is >= 0)
+        G = list(init_rows)
+        k = len(G)
+        AG = A[G]
+        M = AG @ W @ AG.T
+        Mi = np.linalg.pinv(M)
+        lam = Mi @ (b[G] - AG @ x)
+        x = x + W @ AG.T @ lam
+        P = W - W @ AG.T @ Mi @ AG @ W
+        R[:k] = Mi @ AG @ W
+        occ[:k] = True
+        slot_row[:k] = G
+        u[:k] = lam
     rn = 1.0 / np.sqrt(np.einsum("ij,jk,ik->i", A, W, A))
     wscale = np.max(np.diag(W))
     passes = it = drops = multi = 0
@@ -179,7 +194,8 @@ def simulate(H, g, A, b, foot, kmax, tol=1e-9, max_pass=2000, ratio=0.0, stop_af
             u[l] = 0.0
             drops += 1
             cost += 0.6   # H R_l, R (H R_l): two matvecs, two more barriers
-    return dict(passes=passes, it=it, drops=drops, multi=multi, x=x, cost=cost)
+    return dict(passes=passes, it=it, drops=drops, multi=multi, x=x, cost=cost, active=sorted(slot_row[occ].tolist()),
+                u=u[occ])
 
 
 def main():
