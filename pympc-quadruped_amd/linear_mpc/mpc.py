@@ -122,8 +122,15 @@ class ModelPredictiveController():
             # float32 state (quat, pos, omega, vel, R_base), [128, ...) on MPC ticks the
             # gait table f32[4N] and the feet f32[12]
             self._up_bytes = 128 + 4 * (4 * N + 12)
-            self._up_host = np.zeros(self._up_bytes, dtype=np.uint8)
+            # page-locked staging, two buffers: the upload is an asynchronous DMA that the
+            # plan / solve launches queue behind; a buffer is rewritten only after its
+            # previous copy has completed (its event)
+            self._up_pinned = [torch.zeros((self._up_bytes,), dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+            self._up_events = [None, None]
+            self._up_slot = 0
+            self._up_host = self._up_pinned[0].numpy()
             self._up_dev = torch.zeros((self._up_bytes,), dtype=torch.uint8, device=d)
+            self._out_pinned = torch.zeros((12 * N + 2,), dtype=torch.float32, pin_memory=True)
             self._engine = e
         return self._engine
 
@@ -131,7 +138,10 @@ class ModelPredictiveController():
         """Pack the iteration's host inputs (and on MPC ticks the gait table and foot
         positions) into one buffer and copy it to the device in one transfer."""
         import torch
-        h = self._up_host
+        slot = self._up_slot = self._up_slot ^ 1
+        if self._up_events[slot] is not None:
+            self._up_events[slot].synchronize()
+        h = self._up_host = self._up_pinned[slot].numpy()
         lo, nbytes = 0, 120
         if vel_base_des_body is None:   # gait table and feet only (a direct _solve_mpc call)
             lo = 128
@@ -152,7 +162,9 @@ class ModelPredictiveController():
             g[nt:nt + 12] = self._feet_host()
             nbytes = self._up_bytes
         dev = self._up_dev
-        dev[lo:nbytes].copy_(torch.from_numpy(h[lo:nbytes]))
+        dev[lo:nbytes].copy_(self._up_pinned[slot][lo:nbytes], non_blocking=True)
+        ev = self._up_events[slot] = self._up_events[slot] or torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev.device))
         fd = dev[32:120].view(torch.float32)
         v = dict(vb=dev[0:24].view(torch.float64).reshape(1, 3), yr=dev[24:32].view(torch.float64),
                  quat=fd[0:4], pos=fd[4:7], omega=fd[7:10], vel=fd[10:13], rot=fd[13:22])
@@ -265,14 +277,18 @@ class ModelPredictiveController():
 
     def _solve_dev(self, contact, feet, stance, xref=None):
         """The engine call on device buffers: preallocated outputs, one device->host
-        copy (and one synchronisation) for U and the status."""
+        copy (into page-locked memory) and one synchronisation for U and the status."""
+        import torch
         e = self._engine
         dv = self._dev
         # the exact stance count of this table: only the capacity class it needs launches
         e.set_stance_range(stance, stance)
         e.solve_raw(1, dv["x0"], dv["xref"] if xref is None else xref, contact, feet, dv["robot"], dv["u0"],
                     dv["U"], dv["status"], dv["iters"])
-        out = dv["out"].cpu().numpy()
+        out_h = self._out_pinned
+        out_h.copy_(dv["out"], non_blocking=True)
+        torch.cuda.current_stream(dv["out"].device).synchronize()
+        out = out_h.numpy()
         N12 = 12 * self.horizon
         U = out[:N12].astype(np.float64)
         status = int(out[N12:N12 + 1].view(np.int32)[0])
