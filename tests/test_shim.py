@@ -123,6 +123,35 @@ def test_shim_control_loop_matches_oracle():
             assert rel_err_u0(u0, x[:12]) < 1e-4
 
 
+@pytest.mark.gpu
+def test_shim_run_ahead_uploads_keep_every_tick():
+    """Integrator-only ticks neither synchronise nor read back: the page-locked upload
+    buffers alternate, each reused only after its previous copy completed.  A command
+    and a state that change on every one of 47 ticks must integrate exactly as the
+    oracle chain does (a stale or overwritten upload shifts the integrals by a tick's
+    command, ~1e-3)."""
+    from oracle.planner import PlannerOracle, world_velocity
+    m = _shim()
+    c = m.ModelPredictiveController(LinearMpcConfig, AliengoConfig)
+    o = PlannerOracle(10, AliengoConfig.base_height_des)
+    rd = FakeRobotData()
+    table = np.tile(np.array([1, 0, 0, 1], np.float32), 10)
+    for it in range(47):
+        rd.pos_base = np.array([0.0005 * it, 0.0003 * it, 0.37])
+        rd.lin_vel_base = np.array([0.4 + 0.01 * it, 0.05, 0.0])
+        vb = np.array([0.5 + 0.02 * it, 0.1 * np.sin(it), 0.0])
+        yr = 0.05 * np.cos(it)
+        c.update_robot_state(rd)
+        c.update_mpc_if_needed(it, vb, yr, table)
+        o.update_robot_state(np.asarray(rd.quat_base, np.float32), rd.pos_base, rd.ang_vel_base, rd.lin_vel_base)
+        vw = world_velocity(rd.R_base, vb)
+        o.integrate(vw, yr)
+        if it % LinearMpcConfig.iteration_between_mpc == 0:
+            o.reference_trajectory(vw, yr)
+    st = c._planner_state()
+    np.testing.assert_allclose(st[:3], [o.xpos_des, o.ypos_des, o.yaw_des], rtol=0, atol=1e-7)
+
+
 def test_shim_rejects_non_diagonal_weights():
     """mpc.py:50,52 build Qbar = kron(I_N, Q) from a full matrix; the engine's closed
     form needs a diagonal Q / R, so an off-diagonal entry raises (never truncated)."""
