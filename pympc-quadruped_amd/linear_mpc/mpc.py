@@ -131,6 +131,8 @@ class ModelPredictiveController():
             self._up_host = self._up_pinned[0].numpy()
             self._up_dev = torch.zeros((self._up_bytes,), dtype=torch.uint8, device=d)
             self._out_pinned = torch.zeros((12 * N + 2,), dtype=torch.float32, pin_memory=True)
+            self._plan_fns = {}     # xref buffer name -> bound mpcqp_plan launcher
+            self._solve_fns = {}    # (contact, feet, xref) pointers -> bound mpcqp_solve launcher
             self._engine = e
         return self._engine
 
@@ -180,10 +182,16 @@ class ModelPredictiveController():
                           dtype=np.float32).reshape(-1)
 
     def _plan(self, flags, up, xref_key="xref"):
+        """One mpcqp_plan launch on the preallocated buffers (pointers bound once)."""
+        import torch
         e = self._get_engine()
-        dv = self._dev
-        e.plan(flags, dv["plan_state"], dv["x0"], up["vb"], up["yr"], height_des=dv["height"], xref=dv[xref_key],
-               quat=up["quat"], pos=up["pos"], omega=up["omega"], vel=up["vel"], rot=up["rot"])
+        fn = self._plan_fns.get(xref_key)
+        if fn is None:
+            dv = self._dev
+            fn = self._plan_fns[xref_key] = e.bind_plan(
+                dv["plan_state"], dv["x0"], up["vb"], up["yr"], up["quat"], up["pos"], up["omega"], up["vel"],
+                up["rot"], dv["height"], dv[xref_key])
+        fn(flags, torch.cuda.current_stream(e.device))
 
     def _planner_state(self):
         return self._dev["plan_state"].cpu().numpy()[0]
@@ -223,7 +231,6 @@ class ModelPredictiveController():
     def update_mpc_if_needed(self, iter_counter, base_vel_base_des, yaw_turn_rate_des,
                              gait_table, solver='drake', debug=False, iter_debug=None):
         """mpc.py:81-108: integrators on the device every call, a solve on MPC ticks."""
-        from mpcqp._lib import PLAN_REFERENCE
         self._base_vel_base_des = np.asarray(base_vel_base_des, dtype=np.float64).reshape(3)
         self._get_engine()
         if iter_counter % self.iterations_between_mpc == 0:
@@ -231,9 +238,8 @@ class ModelPredictiveController():
             # one upload (state, command, gait table, feet), integrate + reference
             # trajectory in one launch (mpc.py:84-92, :110-170), then the solve
             up = self._upload(self._base_vel_base_des, yaw_turn_rate_des, gait_table)
-            self._plan(PLAN_REFERENCE, up)
+            self.__contact_forces = self._mpc_tick(up)[0:12]
             self.is_first_run = False
-            self.__contact_forces = self._solve_dev(up["contact"], up["feet"], up["stance"])[0:12]
             self._ref_traj_host = None   # ref_traj (mpc.py:97) is read back only when asked for
             if debug and iter_counter == iter_debug:
                 warnings.warn("debug CoM-trajectory plot (mpc.py:293-318) is not provided by the engine")
@@ -281,14 +287,38 @@ class ModelPredictiveController():
         import torch
         e = self._engine
         dv = self._dev
+        fn = self._solve_fn(contact, feet, stance, xref)
+        fn(torch.cuda.current_stream(e.device))
+        self._out_pinned.copy_(dv["out"], non_blocking=True)
+        torch.cuda.current_stream(dv["out"].device).synchronize()
+        return self._read_out()
+
+    def _solve_fn(self, contact, feet, stance, xref=None):
+        """The bound mpcqp_solve launcher for these input buffers (stance range set)."""
+        e = self._engine
+        dv = self._dev
         # the exact stance count of this table: only the capacity class it needs launches
         e.set_stance_range(stance, stance)
-        e.solve_raw(1, dv["x0"], dv["xref"] if xref is None else xref, contact, feet, dv["robot"], dv["u0"],
-                    dv["U"], dv["status"], dv["iters"])
-        out_h = self._out_pinned
-        out_h.copy_(dv["out"], non_blocking=True)
-        torch.cuda.current_stream(dv["out"].device).synchronize()
-        out = out_h.numpy()
+        xr = dv["xref"] if xref is None else xref
+        key = (contact.data_ptr(), feet.data_ptr(), xr.data_ptr())
+        fn = self._solve_fns.get(key)
+        if fn is None:
+            if len(self._solve_fns) > 8:   # host-array xrefs (direct _solve_mpc calls) allocate fresh buffers
+                self._solve_fns.clear()
+            fn = self._solve_fns[key] = e.bind_solve(1, dv["x0"], xr, contact, feet, dv["robot"], dv["u0"],
+                                                     dv["U"], dv["status"], dv["iters"])
+        return fn
+
+    def _mpc_tick(self, up):
+        """An MPC tick after the upload: plan (integrate + reference trajectory) and the
+        solve on the bound launchers, one readback and one synchronisation.  (A HIP graph
+        of the three measured no faster on the GPU pool)"""
+        from mpcqp._lib import PLAN_REFERENCE
+        self._plan(PLAN_REFERENCE, up)
+        return self._solve_dev(up["contact"], up["feet"], up["stance"])
+
+    def _read_out(self):
+        out = self._out_pinned.numpy()
         N12 = 12 * self.horizon
         U = out[:N12].astype(np.float64)
         status = int(out[N12:N12 + 1].view(np.int32)[0])

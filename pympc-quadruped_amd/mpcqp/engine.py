@@ -198,6 +198,20 @@ class LinearMpc:
                                     _ptr(iters), ctypes.c_void_p(stream.cuda_stream))
         _lib.check(self._ctx, code, "mpcqp_solve")
 
+    def bind_solve(self, B, x0, xref, contact, feet, robot, u0, U=None, status=None, iters=None):
+        """solve_raw with its device pointers resolved once: returns ``launch(stream)``.
+        For callers that reuse the same preallocated buffers every tick (the drop-in
+        controller): the per-call cost is then one ctypes call."""
+        lib, ctx = self.lib, self._ctx
+        args = (ctx, int(B), _ptr(x0), _ptr(xref), _ptr(contact), _ptr(feet), _ptr(robot), _ptr(u0), _ptr(U),
+                _ptr(status), _ptr(iters))
+        keep = (x0, xref, contact, feet, robot, u0, U, status, iters)   # the pointers' owners stay alive
+
+        def launch(stream):
+            _lib.check(ctx, lib.mpcqp_solve(*args, ctypes.c_void_p(stream.cuda_stream)), "mpcqp_solve")
+        launch.buffers = keep
+        return launch
+
     # ---- the hot path's callers on the device (include/mpcqp.h, SURVEY §8 f1-f4) ----
 
     def set_planner(self, dt_control=0.001, gravity=9.81, max_pos_error=0.1):
@@ -231,6 +245,22 @@ class LinearMpc:
                 _ptr(vel_body_des), _ptr(yaw_rate_des), _ptr(gait), _ptr(iteration), _ptr(height_des),
                 _ptr(plan_state), _ptr(x0), _ptr(xref), _ptr(contact), s)
         _lib.check(self._ctx, code, "mpcqp_plan")
+
+    def bind_plan(self, plan_state, x0, vel_body_des, yaw_rate_des, quat, pos, omega, vel, rot, height_des,
+                  xref):
+        """plan() (split state inputs) with its device pointers resolved once: returns
+        ``launch(flags, stream)`` (see bind_solve)."""
+        lib, ctx = self.lib, self._ctx
+        B = int(plan_state.shape[0])
+        head = (_ptr(quat), _ptr(pos), _ptr(omega), _ptr(vel), _ptr(rot), _ptr(vel_body_des), _ptr(yaw_rate_des),
+                _ptr(None), _ptr(None), _ptr(height_des), _ptr(plan_state), _ptr(x0), _ptr(xref), _ptr(None))
+        keep = (plan_state, x0, vel_body_des, yaw_rate_des, quat, pos, omega, vel, rot, height_des, xref)
+
+        def launch(flags, stream):
+            _lib.check(ctx, lib.mpcqp_plan(ctx, B, int(flags), *head, ctypes.c_void_p(stream.cuda_stream)),
+                       "mpcqp_plan")
+        launch.buffers = keep
+        return launch
 
     def stance_torques(self, jac, stance, u0, tau, stance_stride=4, stream=None):
         """tau = Jv_leg^T (-f_leg) for stance legs (leg_controller.py:86-89).
