@@ -131,6 +131,8 @@ class ModelPredictiveController():
             self._up_host = self._up_pinned[0].numpy()
             self._up_dev = torch.zeros((self._up_bytes,), dtype=torch.uint8, device=d)
             self._out_pinned = torch.zeros((12 * N + 2,), dtype=torch.float32, pin_memory=True)
+            self._up_pairs = {}     # (slot, lo, nbytes) -> (device slice, pinned slice)
+            self._up_views = None   # device views of the upload buffer's fields
             self._plan_fns = {}     # xref buffer name -> bound mpcqp_plan launcher
             self._solve_fns = {}    # (contact, feet, xref) pointers -> bound mpcqp_solve launcher
             self._engine = e
@@ -163,18 +165,26 @@ class ModelPredictiveController():
             g[:nt] = np.asarray(gait_table, dtype=np.float32).reshape(-1)
             g[nt:nt + 12] = self._feet_host()
             nbytes = self._up_bytes
-        dev = self._up_dev
-        dev[lo:nbytes].copy_(self._up_pinned[slot][lo:nbytes], non_blocking=True)
+        # the (device, pinned) slice pair of this byte range and the device views are
+        # built once: torch view / slice ops cost microseconds each on the host
+        key = (slot, lo, nbytes)
+        pair = self._up_pairs.get(key)
+        if pair is None:
+            pair = self._up_pairs[key] = (self._up_dev[lo:nbytes], self._up_pinned[slot][lo:nbytes])
+        pair[0].copy_(pair[1], non_blocking=True)
         ev = self._up_events[slot] = self._up_events[slot] or torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(dev.device))
-        fd = dev[32:120].view(torch.float32)
-        v = dict(vb=dev[0:24].view(torch.float64).reshape(1, 3), yr=dev[24:32].view(torch.float64),
-                 quat=fd[0:4], pos=fd[4:7], omega=fd[7:10], vel=fd[10:13], rot=fd[13:22])
-        if gait_table is not None:
+        ev.record(torch.cuda.current_stream(self._up_dev.device))
+        v = self._up_views
+        if v is None:
+            dev = self._up_dev
+            fd = dev[32:120].view(torch.float32)
             g = dev[128:self._up_bytes].view(torch.float32)
-            v["contact"] = g[:4 * self.horizon].reshape(1, -1)
-            v["feet"] = g[4 * self.horizon:].reshape(1, 4, 3)
-            v["stance"] = int(np.count_nonzero(h[128:128 + 16 * self.horizon].view(np.float32) > 0))
+            v = self._up_views = dict(
+                vb=dev[0:24].view(torch.float64).reshape(1, 3), yr=dev[24:32].view(torch.float64),
+                quat=fd[0:4], pos=fd[4:7], omega=fd[7:10], vel=fd[10:13], rot=fd[13:22],
+                contact=g[:4 * self.horizon].reshape(1, -1), feet=g[4 * self.horizon:].reshape(1, 4, 3))
+        if gait_table is not None:
+            v = dict(v, stance=int(np.count_nonzero(h[128:128 + 16 * self.horizon].view(np.float32) > 0)))
         return v
 
     def _feet_host(self):
