@@ -43,6 +43,9 @@ constexpr int kMaxN = 20;   // LDS scratch is sized for N <= 20
 #ifndef MPCQP_C64_TW
 #define MPCQP_C64_TW 8   // class-64 register tile width (8: 2 waves per robot; 4: 4 waves, slower)
 #endif
+#ifndef MPCQP_SPLIT_CHOICE
+#define MPCQP_SPLIT_CHOICE 1   // class 64: wave 1 chooses the next rows, wave 0 reads them; 0: both choose
+#endif
 #ifndef MPCQP_SWEEP_MFMA
 #define MPCQP_SWEEP_MFMA 0   // 1: class-64 H^-1 sweep blocked by 4 pivots on the f64 MFMA (parity-exact, slower: DESIGN 4.5)
 #endif

@@ -81,6 +81,7 @@ struct alignas(16) SharedT {
   alignas(16) double tv[Cfg<NV>::VEC];
   alignas(16) double yv[Cfg<NV>::VEC];
   double wmax[Cfg<NV>::NW];
+  int choice;   // class 64, MPCQP_SPLIT_CHOICE: wave 1's published {pass tag, p2 + 1, p + 1}
 };
 
 constexpr int DPP_SHL1 = 0x101;   // row_shl:1 -- lane i reads lane i + 1 (same 16-lane row)
@@ -517,6 +518,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     x[k] = sm.vx[lane + LANES * k];
     u[k] = 0.0;
   }
+  if (tid == 0) sm.choice = 0;   // no pass tag yet (MPCQP_SPLIT_CHOICE)
   fsync<NT>();   // wb, vx and gv are dead: the loop reuses zc / vz / vr2
   unsigned long long occ[VPL];
 #pragma unroll
@@ -548,27 +550,66 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     int p2 = -1, tcA2 = 0, c02 = 0;
     double b0 = 0.0, b1 = 0.0, b2 = 0.0, thr2 = 0.0, sp2 = 0.0;
     if (p < 0) {
-      // most violated row in the dual metric (f32-rounded keys, lowest lane on ties)
-      double key[CPL];
+      // the next row p (and its pair candidate p2): the most violated row in the dual
+      // metric (f32-rounded keys, lowest lane on ties), then the best row of any other
+      // foot-step.  Class 64 with MPCQP_SPLIT_CHOICE: wave 1 -- whose slot rows of R
+      // are idle while <= 32 slots are active -- chooses and publishes {p, p2} in one
+      // pass-tagged LDS word, which wave 0 reads after its R update instead of
+      // repeating both argmins (every decision is identical in both waves, so both
+      // reach every choice point and every exit together).
+      constexpr bool kSplit = MPCQP_SPLIT_CHOICE && NV == 64 && C::NW == 2;
+      int pc = -1, pc2 = -1;
+      if (!kSplit || wave == 1) {
+        double key[CPL];
 #pragma unroll
-      for (int k = 0; k < CPL; ++k)
-        key[k] = s[k] < -tol ? s[k] * (double)(kCurKey ? __builtin_amdgcn_rsqf(fmaxf(qm[k], qfloor)) : qm[k]) : INFINITY;
-      double bv = key[0];
-      int bk = 0;
+        for (int k = 0; k < CPL; ++k)
+          key[k] = s[k] < -tol ? s[k] * (double)(kCurKey ? __builtin_amdgcn_rsqf(fmaxf(qm[k], qfloor)) : qm[k]) : INFINITY;
+        double bv = key[0];
+        int bk = 0;
 #pragma unroll
-      for (int k = 1; k < CPL; ++k) {
-        bk = key[k] < bv ? k : bk;
-        bv = vmin(bv, key[k]);
+        for (int k = 1; k < CPL; ++k) {
+          bk = key[k] < bv ? k : bk;
+          bv = vmin(bv, key[k]);
+        }
+        double kmn;
+        const int pl = wave_argmin_f32(bv, kmn);
+        if (kmn < INFINITY) {
+          pc = pl + LANES * uni(__builtin_amdgcn_readlane(bk, pl));
+          if constexpr (SharedT<NV>::kPair) {
+            const int vc = 3 * (pc / 6);
+            double bw = INFINITY;
+            int bk2 = 0;
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+              const double kk = cz[k] == vc ? INFINITY : key[k];
+              bk2 = kk < bw ? k : bk2;
+              bw = vmin(bw, kk);
+            }
+            double kmn2;
+            const int ql = wave_argmin_f32(bw, kmn2);
+            if (kmn2 < INFINITY) pc2 = ql + LANES * uni(__builtin_amdgcn_readlane(bk2, ql));
+          }
+        }
+        if constexpr (kSplit) {
+          if (lane == 0)
+            *(volatile int*)&sm.choice = (((it + 1) & 0xffff) << 16) | ((pc2 + 1) << 8) | (pc + 1);
+        }
+      } else {
+        const int tag = (it + 1) & 0xffff;
+        int w;
+        do {
+          w = uni(*(volatile int*)&sm.choice);
+        } while ((w >> 16) != tag);
+        pc = (w & 0xff) - 1;
+        pc2 = ((w >> 8) & 0xff) - 1;
       }
-      double kmn;
-      const int pl = wave_argmin_f32(bv, kmn);
-      if (!(kmn < INFINITY)) break;
-      const int kp = uni(__builtin_amdgcn_readlane(bk, pl));
+      if (pc < 0) break;
+      p = pc;
+      const int pl = p & (LANES - 1), kp = p / LANES;
       double sv = s[0];
 #pragma unroll
       for (int k = 1; k < CPL; ++k) sv = (k == kp) ? s[k] : sv;
       const double vmn = readlane_d(sv, pl);
-      p = pl + LANES * kp;
       CNT(4);
       const int rp = p % 6;
       a0 = sgpr_d(sm.mt.rows[rp][0]);
@@ -581,34 +622,21 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       sp = sgpr_d(vmn);   // s_p, tracked like s[] (identical arithmetic)
       up = 0.0;
       SEC(8);
-      // second candidate: the best row of any other foot-step
-      if constexpr (SharedT<NV>::kPair) {
-      double bw = INFINITY;
-      int bk2 = 0;
-#pragma unroll
-      for (int k = 0; k < CPL; ++k) {
-        const double kk = cz[k] == v0 ? INFINITY : key[k];
-        bk2 = kk < bw ? k : bk2;
-        bw = vmin(bw, kk);
-      }
-      double kmn2;
-      const int ql = wave_argmin_f32(bw, kmn2);
-      if (kmn2 < INFINITY) {
-        const int kq = uni(__builtin_amdgcn_readlane(bk2, ql));
+      if (pc2 >= 0) {
+        const int ql = pc2 & (LANES - 1), kq = pc2 / LANES;
         double sv2 = s[0];
 #pragma unroll
         for (int k = 1; k < CPL; ++k) sv2 = (k == kq) ? s[k] : sv2;
         sp2 = sgpr_d(readlane_d(sv2, ql));
-        p2 = ql + LANES * kq;
+        p2 = pc2;
         const int rq = p2 % 6;
         b0 = sgpr_d(sm.mt.rows[rq][0]);
         b1 = sgpr_d(sm.mt.rows[rq][1]);
         b2 = sgpr_d(sm.mt.rows[rq][2]);
         thr2 = sgpr_d(1e-12 * (b0 * b0 + b1 * b1 + b2 * b2) * wscale);
         const int w0 = 3 * (p2 / 6);
-        tcA2 = (int)((unsigned)w0 / TW);   // v0 >= 0: shifts for TW = 8
+        tcA2 = (int)((unsigned)w0 / TW);   // w0 >= 0: shifts for TW = 8
         c02 = (int)((unsigned)w0 % TW);
-      }
       }
     }
     if (++it > max_iter) {
