@@ -56,6 +56,8 @@ def parse():
                     help="diagnostics: one HIP event pair per step (perturbs back-to-back dispatch, "
                          "~5%% slower steps); default: one pair around the timed loop")
     ap.add_argument("--no-callers", action="store_true", help="skip the planner/torque kernel timing")
+    ap.add_argument("--no-hint-line", action="store_true",
+                    help="skip the no_hint sub-line (the default caller path without a stance promise)")
     ap.add_argument("--event-every", type=int, default=8,
                     help="N > 1: bracket every k-th step's solve and gather with HIP events (sampled)")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "latest", "pmc_traffic.json"))
@@ -209,6 +211,13 @@ def rehearse_cpu(args, world, rank, dist):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # every rank's shard size and its synthetic inputs' shapes, checked on rank 0
+    shapes = torch.tensor([Bpg, h["xref"].shape[0], h["xref"].shape[1], h["contact"].shape[0]], dtype=torch.int64)
+    allshapes = [torch.zeros_like(shapes) for _ in range(world)] if world > 1 else [shapes]
+    if world > 1:
+        dist.all_gather(allshapes, shapes)
+    per_rank = [int(t[0]) for t in allshapes]
+    assert all(int(t[1]) == int(t[0]) == int(t[3]) and int(t[2]) == N for t in allshapes), allshapes
     tmax = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -218,6 +227,7 @@ def rehearse_cpu(args, world, rank, dist):
                           "n_gpus": world, "steps": args.steps, "warmup": 0, "rehearsal": True,
                           "note": "gloo rehearsal on CPU tensors: stand-in solve (zero fill), not a measurement",
                           "gathered_rows": rows, "gather_ok": gather_ok, "x0_rows": int(x0.shape[0]),
+                          "per_rank_batch": per_rank, "horizon": N,
                           "config": {"workload": f"{args.config}: {total} robots over {world} ranks",
                                      "global_batch": total,
                                      "parallelism": f"robot-sharded x{world} + gloo all-gather of u0"}}))
@@ -451,8 +461,12 @@ def main():
     for k in range(nbat):
         it = iters[k].cpu().numpy()
         ns = 3 * (host[k]["contact"] > 0).reshape(Bpg, -1).sum(1)
-        flops_launch.append(sum(algorithmic_flops(N, int(n), int(i)) for n, i in zip(ns, it)))
-        exec_launch.append(sum(executed_flops(N, int(n), int(i)) for n, i in zip(ns, it)))
+        # iters of an interior-point robot (n > 128) count Newton factorisations, not
+        # active-set steps: such robots are priced at the formulation + one n^3/3
+        # factorisation only (K = 0), a lower bound on their work
+        ki = [0 if n > 128 else int(i) for n, i in zip(ns, it)]
+        flops_launch.append(sum(algorithmic_flops(N, int(n), k) for n, k in zip(ns, ki)))
+        exec_launch.append(sum(executed_flops(N, int(n), k) for n, k in zip(ns, ki)))
         it_all.append(it)
     st = np.concatenate([x.cpu().numpy() for x in status])   # every batch's last solve
     steps_per_bat = [sum(1 for s in range(args.steps) if s % nbat == k) for k in range(nbat)]
@@ -463,17 +477,58 @@ def main():
     it_all = np.concatenate(it_all)
 
     qps = world * Bpg * args.steps / elapsed
-    traffic = None
+    # HBM traffic cannot be counted inside this process (PMC needs a rocprofv3 pass of its
+    # own): it is attached only from a profile of THIS build (library SHA-256 match) of
+    # the same config and batch, with its provenance; otherwise null
+    traffic, traffic_source, traffic_note = None, None, None
     try:
+        from mpcqp import _lib as _mlib
         with open(args.pmc_file) as fh:
             pmc = json.load(fh)
         entry = pmc.get(args.config)
-        if entry and entry.get("batch") == Bpg:
+        sha = _mlib.lib_sha256()
+        if not entry or entry.get("batch") != Bpg:
+            traffic_note = f"no PMC profile of {args.config} at batch {Bpg} in {os.path.relpath(args.pmc_file, ROOT)}"
+        elif entry.get("lib_sha256") != sha:
+            traffic_note = (f"the PMC profile in {os.path.relpath(args.pmc_file, ROOT)} was taken on another build "
+                            f"(lib {str(entry.get('lib_sha256'))[:12]} != {sha[:12]}): not attached")
+        else:
             traffic = entry.get("hbm_bytes_per_launch")
-    except Exception:
-        traffic = None
+            kern = entry.get("kernels", {}).get(entry.get("dominant_kernel"), {})
+            traffic_source = {"file": os.path.relpath(args.pmc_file, ROOT), "profile_dir": entry.get("profile_dir"),
+                              "lib_sha256": sha, "kernel": entry.get("dominant_kernel"),
+                              "fetch_kib_raw": kern.get("fetch_kib_per_launch_raw"),
+                              "write_kib": kern.get("write_kib_per_launch"),
+                              "formula": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM; the x2 is the "
+                                         "guide's 16-B/lane stream calibration, uncalibrated for this kernel's "
+                                         "per-robot slices)",
+                              "measured_by": "separate rocprofv3 --pmc passes (tools/profile.sh), not this run"}
+    except Exception as exc:   # noqa: BLE001 -- provenance is best effort, never fatal
+        traffic_note = f"traffic unavailable: {exc}"
 
     callers = None if args.no_callers else time_callers(eng, host[0], Bpg, N, dev, stream)
+    # the default caller path (no stance promise: every capacity class launched, the idle
+    # workgroups of the queued classes exit at once), timed the same way, outside `value`
+    no_hint = None
+    if not args.no_hint_line and world == 1:
+        eng.set_stance_range(0, 0)
+        for k in range(5):
+            step(k)
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        nh_steps = min(args.steps, 50)
+        t1 = time.perf_counter()
+        e0.record(stream)
+        for k in range(nh_steps):
+            step(k)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        nh_el = time.perf_counter() - t1
+        no_hint = {"max_stance": 0, "steps": nh_steps, "value": Bpg * nh_steps / nh_el, "unit": "QP/s",
+                   "ms_per_step": nh_el / nh_steps * 1e3, "kernel_ms_avg": e0.elapsed_time(e1) / nh_steps,
+                   "vs_hinted": (Bpg * nh_steps / nh_el) / qps,
+                   "note": "LinearMpc(max_stance=0): the caller promises nothing about its schedules"}
+        eng.set_stance_hint(max_stance)
     gather_ms = (sum(a.elapsed_time(b) for a, b in gather_events) / len(gather_events)
                  if gather_events else None)
 
@@ -516,6 +571,7 @@ def main():
             # the path (gfx950's FP64 MFMA peak equals its FP64 VALU peak)
             "roofline": {"bound": "valu", "pipe": "fp64 VALU", "achieved": achieved, "peak": PEAK_FP64_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic,
+                         "traffic_source": traffic_source,
                          "executed_frac": E_avg / kavg_s / 1e12 / PEAK_FP64_TFLOPS},
             "cpu_baseline": cpu,
             "kernel_ms_avg": kavg_s * 1e3,
@@ -525,6 +581,10 @@ def main():
             "status_ok_frac": float((st == 0).mean()),
             "callers": callers,
         }
+        if traffic_note:
+            line["roofline"]["traffic_note"] = traffic_note
+        if no_hint is not None:
+            line["no_hint"] = no_hint
         if gather_ms is not None:
             line["gather_ms_avg"] = gather_ms
         if args.standing_every:

@@ -36,7 +36,15 @@
  *   u0      [B][12]    out: first-step GRFs, world frame (mpc.py:99)
  *   U       [B][N][12] out (nullable): the whole optimal input sequence
  *   status  [B]        out (nullable): MPCQP_STATUS_*
- *   iters   [B]        out (nullable): active-set steps executed (a pair step counts 2)
+ *   iters   [B]        out (nullable): active-set steps executed (a pair step counts 2);
+ *                      for a robot with more than 128 stance variables (the interior-point
+ *                      class: standing schedules at N >= 11) the Newton factorisations
+ *
+ * Input reads: a robot's x0 / xref / contact / feet / robot slices are staged with
+ * 16-byte loads of the 16-byte-aligned chunks that cover them, so up to 12 bytes
+ * before and after each slice (never across a 4 KiB page) are read and ignored.
+ * The buffers must be device allocations (hipMalloc / torch: page-granular, no
+ * guard pages); the values read outside a slice never reach any result.
  */
 #ifndef MPCQP_H
 #define MPCQP_H
@@ -49,7 +57,8 @@ extern "C" {
 
 #define MPCQP_ABI_VERSION 3
 #define MPCQP_ROBOT_STRIDE 16
-#define MPCQP_MAX_HORIZON 32
+#define MPCQP_MAX_HORIZON 20   /* mpcqp_create rejects horizon > 20 (MPCQP_ERR_ARG): the
+                                  per-robot LDS scratch of every class is sized for it */
 
 /* error codes (return values) */
 #define MPCQP_OK 0
@@ -70,7 +79,9 @@ extern "C" {
 
 typedef struct mpcqp_params {
   int32_t horizon;       /* N (LinearMpcConfig.horizon, linear_mpc_configs.py:11) */
-  int32_t max_iter;      /* active-set iteration cap per robot, 0 = default */
+  int32_t max_iter;      /* active-set iteration cap per robot of the dense classes (n <= 126),
+                            0 = default; the interior-point class (n > 128) stops after its own
+                            60 Newton iterations and does not read it */
   double dt;             /* model step, 0.05 in the reference (mpc.py:38) */
   double q_diag[13];     /* state weights (linear_mpc_configs.py:19) */
   double r_diag[12];     /* input weights (linear_mpc_configs.py:20) */
@@ -97,7 +108,9 @@ int mpcqp_set_stance_hint(mpcqp_ctx* ctx, int32_t max_stance);
  * classes no robot can need are not launched, and when the range rules out the
  * smaller classes the first possible one takes the batch directly (the drop-in
  * controller passes its gait table's exact count).  A robot outside the range is
- * still solved if a launched class covers it, else reports MPCQP_STATUS_TOO_LARGE. */
+ * still solved if a launched class covers it, else reports MPCQP_STATUS_TOO_LARGE.
+ * MPCQP_ERR_ARG when min_stance > 4 * horizon (no schedule has that many) or
+ * min_stance > max_stance > 0. */
 int mpcqp_set_stance_range(mpcqp_ctx* ctx, int32_t min_stance, int32_t max_stance);
 
 /* ---- the hot path's callers on the device -------------

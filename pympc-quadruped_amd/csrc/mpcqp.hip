@@ -39,7 +39,8 @@ namespace {
 constexpr int NX = 13;      // state dimension (mpc.py:26)
 constexpr int NU = 12;      // input dimension (mpc.py:28)
 constexpr int LANES = 64;
-constexpr int kMaxN = 20;   // LDS scratch is sized for N <= 20
+constexpr int kMaxN = MPCQP_MAX_HORIZON;   // LDS scratch is sized for N <= 20 (include/mpcqp.h)
+static_assert(kMaxN == 20, "the dense classes' and the interior-point class's LDS layouts are sized for N <= 20");
 #ifndef MPCQP_C64_TW
 #define MPCQP_C64_TW 8   // class-64 register tile width (8: 2 waves per robot; 4: 4 waves, slower)
 #endif
@@ -425,6 +426,7 @@ struct QueueSet {
   hipStream_t stream;
   int cap;
   int* buf;
+  unsigned long long used;   // last use (LRU eviction beyond kMaxQueueSets streams)
 };
 
 struct mpcqp_ctx {
@@ -434,6 +436,7 @@ struct mpcqp_ctx {
   int stance_min;    // min stance foot-steps per robot promised by the caller
   int ncu;
   std::vector<QueueSet> queues;
+  unsigned long long use_clock;
   double dt_control;  // planner constants (mpcqp_set_planner)
   double gravity;
   double max_pos_error;
@@ -458,6 +461,11 @@ struct DeviceScope {
   }
 };
 
+// At most this many streams keep a queue set; a new stream beyond them takes over the
+// least recently used set (after a device synchronisation: its stream may still run
+// launches that use it, and may already have been destroyed by the caller).
+constexpr int kMaxQueueSets = 8;
+
 // The queue set of `st`, holding at least `batch` robots per queue (grown on demand;
 // the old buffer is freed once the stream's earlier launches are done).
 static int* stream_queues(mpcqp_ctx* ctx, hipStream_t st, int batch, int* err, int* cap) {
@@ -465,12 +473,25 @@ static int* stream_queues(mpcqp_ctx* ctx, hipStream_t st, int batch, int* err, i
   QueueSet* qs = nullptr;
   for (auto& q : ctx->queues)
     if (q.stream == st) qs = &q;
+  if (qs) qs->used = ++ctx->use_clock;
   if (qs && qs->cap >= batch) {
     *cap = qs->cap;
     return qs->buf;
   }
+  if (!qs && (int)ctx->queues.size() >= kMaxQueueSets) {
+    QueueSet* lru = &ctx->queues[0];
+    for (auto& q : ctx->queues)
+      if (q.used < lru->used) lru = &q;
+    if (hipDeviceSynchronize() != hipSuccess) {
+      *err = set_err(ctx, MPCQP_ERR_HIP, "queue eviction: device sync failed");
+      return nullptr;
+    }
+    (void)hipFree(lru->buf);
+    *lru = QueueSet{st, 0, nullptr, ++ctx->use_clock};
+    qs = lru;
+  }
   if (!qs) {
-    ctx->queues.push_back(QueueSet{st, 0, nullptr});
+    ctx->queues.push_back(QueueSet{st, 0, nullptr, ++ctx->use_clock});
     qs = &ctx->queues.back();
   }
   if (qs->buf) {
@@ -526,6 +547,7 @@ int mpcqp_create(const mpcqp_params* p, int32_t device, mpcqp_ctx** out) {
   ctx->stance_hint = 0;
   ctx->stance_min = 0;
   ctx->ncu = 0;
+  ctx->use_clock = 0;
   ctx->dt_control = 0.001;    // linear_mpc_configs.py:6
   ctx->gravity = 9.81;        // linear_mpc_configs.py:13
   ctx->max_pos_error = 0.1;   // mpc.py:121
@@ -541,7 +563,13 @@ int mpcqp_set_stance_hint(mpcqp_ctx* ctx, int32_t max_stance) {
 }
 
 int mpcqp_set_stance_range(mpcqp_ctx* ctx, int32_t min_stance, int32_t max_stance) {
-  if (!ctx || min_stance < 0 || max_stance < 0 || (max_stance > 0 && min_stance > max_stance)) return MPCQP_ERR_ARG;
+  if (!ctx) return MPCQP_ERR_ARG;
+  if (min_stance < 0 || max_stance < 0 || (max_stance > 0 && min_stance > max_stance))
+    return set_err(ctx, MPCQP_ERR_ARG, "stance range: min > max or negative");
+  // a schedule has at most 4 N stance foot-steps: a larger minimum would route the whole
+  // batch past every class mpcqp_solve launches (and leave the outputs unwritten)
+  if (min_stance > 4 * ctx->params.horizon)
+    return set_err(ctx, MPCQP_ERR_ARG, "stance range: min_stance > 4 * horizon");
   ctx->stance_min = min_stance;
   ctx->stance_hint = max_stance;
   return MPCQP_OK;
@@ -696,11 +724,10 @@ int mpcqp_stance_torques(mpcqp_ctx* ctx, int32_t batch, const float* jac, const 
 int mpcqp_destroy(mpcqp_ctx* ctx) {
   if (ctx) {
     DeviceScope dev(ctx->device);
+    // hipFree synchronises the device before releasing the memory: no per-stream sync
+    // (a recorded stream may already have been destroyed by the caller)
     for (auto& q : ctx->queues)
-      if (q.buf) {
-        (void)hipStreamSynchronize(q.stream);
-        (void)hipFree(q.buf);
-      }
+      if (q.buf) (void)hipFree(q.buf);
   }
   delete ctx;
   return MPCQP_OK;

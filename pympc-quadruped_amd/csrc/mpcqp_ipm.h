@@ -154,6 +154,10 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
   form_stance(smf, sm.mt, N, lane);
   fsync<NT>();
   const int S = uni(sm.mt.S);
+  if (S == 0) {   // no stance foot-step (a caller's promise broken by a flight schedule): U = 0
+    write_empty_t<NT>(b, lane, N, MPCQP_STATUS_OK, u0g, Ug, statusg, itersg);
+    return;
+  }
   form_model<NT>(KP, smf, sm.fa.fy, sm.mt, N, lane);
   fsync<NT>();
   {

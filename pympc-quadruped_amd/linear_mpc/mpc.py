@@ -80,6 +80,10 @@ class ModelPredictiveController():
         self.iterations_between_mpc = mpc_config.iteration_between_mpc
         self.dt = 0.05
         self.horizon = mpc_config.horizon
+        from mpcqp import _lib
+        if not 1 <= int(self.horizon) <= _lib.MAX_HORIZON:
+            raise ValueError(f"LinearMpcConfig.horizon = {self.horizon}: the MI355X engine supports "
+                             f"1..{_lib.MAX_HORIZON} (MPCQP_MAX_HORIZON, include/mpcqp.h)")
         self.mu = mpc_config.friction_coef
         self.fz_max = robot_config.fz_max
         self.gravity = mpc_config.gravity

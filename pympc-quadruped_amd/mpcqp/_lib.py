@@ -18,6 +18,7 @@ STATUS_INFEASIBLE = 2
 STATUS_TOO_LARGE = 3
 STATUS_NONFINITE = 4
 ROBOT_STRIDE = 16
+MAX_HORIZON = 20    # MPCQP_MAX_HORIZON: mpcqp_create rejects a longer horizon
 
 # every symbol declared in include/mpcqp.h
 EXPORTED_SYMBOLS = (
@@ -103,6 +104,13 @@ def default_params(horizon):
     p = MpcqpParams()
     load().mpcqp_default_params(ctypes.byref(p), int(horizon))
     return p
+
+
+def lib_sha256(path=None):
+    """SHA-256 of the engine library file (ties a profile's counters to the build that made them)."""
+    import hashlib
+    with open(path or LIB_PATH, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()
 
 
 def check(ctx, code, what):

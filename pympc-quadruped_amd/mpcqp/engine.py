@@ -61,6 +61,9 @@ class LinearMpc:
     def __init__(self, horizon=16, robot="aliengo", dt=DT_MPC, Q=Q_DIAG, R=R_DIAG,
                  device="cuda:0", max_iter=0, max_stance=0):
         self.horizon = int(horizon)
+        if not 1 <= self.horizon <= _lib.MAX_HORIZON:
+            raise ValueError(f"horizon {self.horizon} outside the engine's 1..{_lib.MAX_HORIZON} "
+                             "(MPCQP_MAX_HORIZON, include/mpcqp.h)")
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise ValueError("LinearMpc runs on a HIP device only (no CPU path)")

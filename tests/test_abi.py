@@ -73,6 +73,27 @@ def test_header_constants_match_binding():
     assert int(consts["MPCQP_ROBOT_STRIDE"]) == _lib.ROBOT_STRIDE
 
 
+def test_horizon_limit_is_the_create_limit():
+    """MPCQP_MAX_HORIZON (include/mpcqp.h) is exactly what mpcqp_create accepts (the
+    horizon check runs before any HIP call), and the Python surfaces raise on a longer
+    horizon with the limit in the message (linear_mpc_configs.py:11 is a free value)."""
+    from mpcqp import _lib, LinearMpc
+    src = open(HEADER).read()
+    limit = int(re.search(r"#define MPCQP_MAX_HORIZON (\d+)", src).group(1))
+    assert limit == _lib.MAX_HORIZON == 20
+    lib = _lib.load()
+    ctx = ctypes.c_void_p()
+    p = _lib.default_params(limit + 1)
+    assert lib.mpcqp_create(ctypes.byref(p), 0, ctypes.byref(ctx)) == -1   # MPCQP_ERR_ARG
+    p = _lib.default_params(limit)
+    rc = lib.mpcqp_create(ctypes.byref(p), 0, ctypes.byref(ctx))
+    assert rc != -1   # accepted (no GPU here: MPCQP_ERR_HIP from the device query)
+    if rc == 0:
+        lib.mpcqp_destroy(ctx)
+    with pytest.raises(ValueError, match="1..20"):
+        LinearMpc(horizon=limit + 1, device="cuda:0")
+
+
 def test_gait_records_are_the_reference_gaits():
     """gait.py:16-22 member names -> [period, offsets, durations]."""
     from mpcqp.params import gait_record

@@ -1,4 +1,5 @@
-"""CPU, world_size 2 over gloo: the multi-GPU path (shard + end-of-step u0 gather)."""
+"""CPU over gloo: the multi-GPU path (shard + end-of-step u0 gather) at world sizes
+2 and 8 -- the 8-GPU node's rank count, at the bench configs' global totals."""
 import os
 import socket
 
@@ -69,3 +70,33 @@ def test_bench_spawns_its_own_ranks(total):
     assert line["n_gpus"] == 2 and line["rehearsal"] is True
     assert line["gathered_rows"] == total and line["gather_ok"] is True
     assert line["config"]["global_batch"] == total
+
+
+@pytest.mark.parametrize("config,total", [("config4", 0), ("config5", 0), ("config4", 16381), ("config2", 8191)])
+def test_bench_rehearsal_world8(config, total):
+    """`bench.py --gpus 8 --rehearse-cpu`: eight gloo ranks, each building its shard of the
+    config's real workload (CONFIGS[config]: batch per GPU, horizon, gaits, robots; config
+    4: 8 x 2048 = 16 384 robots at N = 16, config 5: 8 x 8192 = 65 536 at N = 20) or of an
+    uneven global total, then the u0 all-gather: every robot's row arrives in global order
+    on rank 0 (the loop it replaces is isaacgym_a1.py:119-164)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    from mpcqp.dist import shard
+    bpg, N = bench.CONFIGS[config][0], bench.CONFIGS[config][1]
+    world = 8
+    want_total = total or world * bpg
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", str(world), "--rehearse-cpu",
+           "--config", config, "--steps", "2"] + (["--total", str(total)] if total else [])
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, check=True)
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == world and line["gathered_rows"] == want_total and line["gather_ok"] is True
+    assert line["config"]["global_batch"] == want_total and line["horizon"] == N
+    assert line["per_rank_batch"] == [shard(want_total, r, world)[1] for r in range(world)]

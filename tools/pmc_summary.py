@@ -73,8 +73,12 @@ def main():
                              hbm_bytes_per_launch=(2 * fk * 1024 + wk * 1024) if fk is not None and wk is not None
                              else None)
     dom = per_kernel.get(dominant, {})
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "pympc-quadruped_amd"))
+    from mpcqp import _lib
     entry = {
         "batch": batch,
+        "lib_sha256": _lib.lib_sha256(),   # the build these counters belong to (bench.py checks it)
+        "profile_dir": dst,
         "dominant_kernel": dominant,
         "kernel_avg_ns_rocprof": dom.get("avg_ns"),
         "kernel_ms_avg_bench_events": bench.get("kernel_ms_avg"),
