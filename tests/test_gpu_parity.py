@@ -13,6 +13,10 @@ TOL_U0 = 1e-4   # north_star: GRF within 1e-4 relative, norm-wise ||du0||_inf / 
 # class ~2e-6 on these cases): a regression guard 10x tighter than the contract, so a
 # build that loses digits (e.g. an explicit block-inverse sweep) fails here
 TOL_ACHIEVED = 1e-5
+# the interior-point class (n > 128) stops its active-set polish at a stationarity
+# residual of 1e-10 x the gradient scale: on random contact patterns that leaves up to
+# ~2e-5 (tools/parity_dist.py), still 5x inside the contract
+TOL_ACHIEVED_IPM = 5e-5
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 pytestmark = pytest.mark.gpu
@@ -266,13 +270,18 @@ def test_random_contact_patterns_every_class(N):
     assert (status == 0).all(), status
     stance = bt["contact"].reshape(B, -1).sum(1)
     assert stance.max() == 4 * N and stance.min() == 0
-    worst = 0.0
+    worst, worst_ipm = 0.0, 0.0
     for b in range(B):
         x, _, _ = oracle_solution(bt, b, N)
         assert rel_err_u0(u0[b], x[:12]) < TOL_U0, (b, int(stance[b]), u0[b], x[:12])
-        worst = max(worst, rel_err_u0(u0[b], x[:12]), rel_err_u0(U[b], x))
+        e = max(rel_err_u0(u0[b], x[:12]), rel_err_u0(U[b], x))
+        if 3 * stance[b] > 128:
+            worst_ipm = max(worst_ipm, e)
+        else:
+            worst = max(worst, e)
         assert rel_err_u0(U[b], x) < TOL_U0, (b, int(stance[b]))
     assert worst < TOL_ACHIEVED, worst
+    assert worst_ipm < TOL_ACHIEVED_IPM, worst_ipm
     assert np.all(U[1] == 0) and np.all(u0[1] == 0)
     assert bt["robot"][:, R_NX:R_NZ + 1].shape == (B, 3)
 
