@@ -50,6 +50,9 @@ static_assert(kMaxN == 20, "the dense classes' and the interior-point class's LD
 #ifndef MPCQP_SWEEP_MFMA
 #define MPCQP_SWEEP_MFMA 0   // 1: class-64 H^-1 sweep blocked by 4 pivots on the f64 MFMA (parity-exact, slower: DESIGN 4.5)
 #endif
+#ifndef MPCQP_BM
+#define MPCQP_BM 0   // 1: class 64 as a brain / muscle pair of waves (mpcqp_bm.h, measured slower: DESIGN 4.5)
+#endif
 #ifndef MPCQP_C64_WPE
 #define MPCQP_C64_WPE (MPCQP_C64_TW == 4 ? 4 : 2)   // class-64 waves per SIMD (VGPR budget)
 #endif
@@ -300,6 +303,7 @@ __device__ __forceinline__ int wave_argmin_f32(double v, double& vmin_out) {
 #include "mpcqp_form.h"
 #include "mpcqp_sweep_mfma.h"
 #include "mpcqp_solve.h"
+#include "mpcqp_bm.h"
 #include "mpcqp_ipm.h"
 #include "mpcqp_plan.h"
 
@@ -322,11 +326,17 @@ __global__ __launch_bounds__(Cfg<64>::NT) __attribute__((amdgpu_waves_per_eu(MPC
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
     int* __restrict__ queue, int* __restrict__ queue_big, int* __restrict__ queue_ipm) {
-  __shared__ SharedT<64> sm;
   if ((int)blockIdx.x >= B) return;
   const int b = xcd_robot(blockIdx.x, B);
+#if MPCQP_BM
+  __shared__ SharedBM sm;
+  solve_robot_bm(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, queue, queue_big,
+                 queue_ipm);
+#else
+  __shared__ SharedT<64> sm;
   solve_robot<64>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, queue, queue_big,
                   queue_ipm);
+#endif
 }
 
 // Class NV = 96: one 6-wave workgroup (4 x 6 register tiles) per robot queued by
@@ -427,7 +437,22 @@ struct QueueSet {
   int cap;
   int* buf;
   unsigned long long used;   // last use (LRU eviction beyond kMaxQueueSets streams)
+  // the interior-point class runs on a side stream forked from `stream` after the first
+  // (routing) class and joined back at the end of the call (created on first use)
+  hipStream_t side;
+  hipEvent_t ev_fork, ev_join;
 };
+
+// Releases a queue set's device resources (the caller has synchronised the device).
+static void release_set(QueueSet& q) {
+  if (q.buf) (void)hipFree(q.buf);
+  if (q.ev_fork) (void)hipEventDestroy(q.ev_fork);
+  if (q.ev_join) (void)hipEventDestroy(q.ev_join);
+  if (q.side) (void)hipStreamDestroy(q.side);
+  q.buf = nullptr;
+  q.ev_fork = q.ev_join = nullptr;
+  q.side = nullptr;
+}
 
 struct mpcqp_ctx {
   mpcqp_params params;
@@ -468,7 +493,7 @@ constexpr int kMaxQueueSets = 8;
 
 // The queue set of `st`, holding at least `batch` robots per queue (grown on demand;
 // the old buffer is freed once the stream's earlier launches are done).
-static int* stream_queues(mpcqp_ctx* ctx, hipStream_t st, int batch, int* err, int* cap) {
+static QueueSet* stream_queues(mpcqp_ctx* ctx, hipStream_t st, int batch, int* err, int* cap) {
   *err = MPCQP_OK;
   QueueSet* qs = nullptr;
   for (auto& q : ctx->queues)
@@ -476,7 +501,7 @@ static int* stream_queues(mpcqp_ctx* ctx, hipStream_t st, int batch, int* err, i
   if (qs) qs->used = ++ctx->use_clock;
   if (qs && qs->cap >= batch) {
     *cap = qs->cap;
-    return qs->buf;
+    return qs;
   }
   if (!qs && (int)ctx->queues.size() >= kMaxQueueSets) {
     QueueSet* lru = &ctx->queues[0];
@@ -486,12 +511,12 @@ static int* stream_queues(mpcqp_ctx* ctx, hipStream_t st, int batch, int* err, i
       *err = set_err(ctx, MPCQP_ERR_HIP, "queue eviction: device sync failed");
       return nullptr;
     }
-    (void)hipFree(lru->buf);
-    *lru = QueueSet{st, 0, nullptr, ++ctx->use_clock};
+    release_set(*lru);
+    *lru = QueueSet{st, 0, nullptr, ++ctx->use_clock, nullptr, nullptr, nullptr};
     qs = lru;
   }
   if (!qs) {
-    ctx->queues.push_back(QueueSet{st, 0, nullptr, ++ctx->use_clock});
+    ctx->queues.push_back(QueueSet{st, 0, nullptr, ++ctx->use_clock, nullptr, nullptr, nullptr});
     qs = &ctx->queues.back();
   }
   if (qs->buf) {
@@ -515,7 +540,24 @@ static int* stream_queues(mpcqp_ctx* ctx, hipStream_t st, int batch, int* err, i
   }
   qs->cap = batch;
   *cap = batch;
-  return qs->buf;
+  return qs;
+}
+
+// The side stream and fork / join events of a queue set (created on first use).
+static bool side_stream(QueueSet* qs) {
+  if (!qs->side && hipStreamCreateWithFlags(&qs->side, hipStreamNonBlocking) != hipSuccess) {
+    qs->side = nullptr;
+    return false;
+  }
+  if (!qs->ev_fork && hipEventCreateWithFlags(&qs->ev_fork, hipEventDisableTiming) != hipSuccess) {
+    qs->ev_fork = nullptr;
+    return false;
+  }
+  if (!qs->ev_join && hipEventCreateWithFlags(&qs->ev_join, hipEventDisableTiming) != hipSuccess) {
+    qs->ev_join = nullptr;
+    return false;
+  }
+  return true;
 }
 
 extern "C" {
@@ -605,40 +647,66 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   // the first class launched: 0 = class 64, 1 = 96, 2 = 128, 3 = interior point
   const int first = nmin > 128 ? 3 : nmin > 96 ? 2 : nmin > 64 ? 1 : 0;
   int* q = nullptr;
+  QueueSet* qs = nullptr;
   int cap = 0;
   if (large) {
     int qerr = MPCQP_OK;
-    q = stream_queues(ctx, st, batch, &qerr, &cap);
-    if (!q) return qerr;
+    qs = stream_queues(ctx, st, batch, &qerr, &cap);
+    if (!qs) return qerr;
+    q = qs->buf;
   }
+  // the interior-point class (one wave per robot, latency-bound) on a side stream as soon
+  // as the first class has routed its robots, beside classes 96 / 128 instead of behind
+  // them; the caller's stream waits for it at the end of the call
+  const bool fork = giant && first < 3 && side_stream(qs);
+  bool ipm_done = false;
+  auto launch_ipm = [&](hipStream_t s) -> hipError_t {
+    hipLaunchKernelGGL(mpcqp_kernel_ipm, dim3(batch), dim3(LANES), 0, s, kp, x0, xref, contact, feet, robot, u0, U,
+                       (int*)status, (int*)iters, q + 2 * (4 + (size_t)cap), first == 3 ? (int)batch : 0);
+    ipm_done = true;
+    return hipGetLastError();
+  };
+  auto fork_ipm = [&]() -> int {
+    if (!fork || ipm_done) return MPCQP_OK;
+    if (hipEventRecord(qs->ev_fork, st) != hipSuccess || hipStreamWaitEvent(qs->side, qs->ev_fork, 0) != hipSuccess)
+      return set_err(ctx, MPCQP_ERR_HIP, "interior-point fork failed");
+    const hipError_t le = launch_ipm(qs->side);
+    if (le != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (ipm): ") + hipGetErrorString(le));
+    if (hipEventRecord(qs->ev_join, qs->side) != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, "join record failed");
+    return MPCQP_OK;
+  };
   const size_t qstride = 4 + (size_t)cap;   // the set's layout: three queues of 4 + cap ints
   int* q1 = large ? q : nullptr;
   int* q2 = huge ? q + qstride : nullptr;
   int* q3 = giant ? q + 2 * qstride : nullptr;
   hipError_t e = hipSuccess;
+  int fe = MPCQP_OK;
   if (first == 0) {
     hipLaunchKernelGGL(mpcqp_kernel_64, dim3(batch), dim3(Cfg<64>::NT), 0, st, kp, (int)batch, x0, xref, contact,
                        feet, robot, u0, U, (int*)status, (int*)iters, q1, q2, q3);
     e = hipGetLastError();
     if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch: ") + hipGetErrorString(e));
+    if ((fe = fork_ipm()) != MPCQP_OK) return fe;
   }
   if (large && first <= 1) {
     hipLaunchKernelGGL(mpcqp_kernel_96, dim3(batch), dim3(Cfg<96>::NT), 0, st, kp, x0, xref, contact, feet, robot,
                        u0, U, (int*)status, (int*)iters, q1, q2, q3, first == 1 ? (int)batch : 0);
     e = hipGetLastError();
     if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (96): ") + hipGetErrorString(e));
+    if ((fe = fork_ipm()) != MPCQP_OK) return fe;
   }
   if (huge && first <= 2) {
     hipLaunchKernelGGL(mpcqp_kernel_128, dim3(batch), dim3(Cfg<128>::NT), 0, st, kp, x0, xref, contact, feet, robot,
                        u0, U, (int*)status, (int*)iters, q2, q3, first == 2 ? (int)batch : 0);
     e = hipGetLastError();
     if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (128): ") + hipGetErrorString(e));
+    if ((fe = fork_ipm()) != MPCQP_OK) return fe;
   }
-  if (giant) {
-    hipLaunchKernelGGL(mpcqp_kernel_ipm, dim3(batch), dim3(LANES), 0, st, kp, x0, xref, contact, feet, robot, u0, U,
-                       (int*)status, (int*)iters, q3, first == 3 ? (int)batch : 0);
-    e = hipGetLastError();
+  if (giant && !ipm_done) {   // the interior-point class takes the batch directly (or no side stream)
+    e = launch_ipm(st);
     if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (ipm): ") + hipGetErrorString(e));
+  } else if (fork && hipStreamWaitEvent(st, qs->ev_join, 0) != hipSuccess) {
+    return set_err(ctx, MPCQP_ERR_HIP, "interior-point join failed");
   }
   return MPCQP_OK;
 }
@@ -726,8 +794,7 @@ int mpcqp_destroy(mpcqp_ctx* ctx) {
     DeviceScope dev(ctx->device);
     // hipFree synchronises the device before releasing the memory: no per-stream sync
     // (a recorded stream may already have been destroyed by the caller)
-    for (auto& q : ctx->queues)
-      if (q.buf) (void)hipFree(q.buf);
+    for (auto& q : ctx->queues) release_set(q);
   }
   delete ctx;
   return MPCQP_OK;
