@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define MPCQP_ABI_VERSION 3
+#define MPCQP_ABI_VERSION 4
 #define MPCQP_ROBOT_STRIDE 16
 #define MPCQP_MAX_HORIZON 20   /* mpcqp_create rejects horizon > 20 (MPCQP_ERR_ARG): the
                                   per-robot LDS scratch of every class is sized for it */
@@ -76,6 +76,8 @@ extern "C" {
 #define MPCQP_STATUS_INFEASIBLE 2  /* cannot happen for this QP (U = 0 is feasible) */
 #define MPCQP_STATUS_TOO_LARGE 3   /* stance variables exceed the engine's capacity */
 #define MPCQP_STATUS_NONFINITE 4   /* non-finite input or result */
+#define MPCQP_STATUS_UNSUPPORTED 5 /* weights the robot's capacity class cannot apply (see
+                                      mpcqp_set_weights); u0 / U are 0 */
 
 typedef struct mpcqp_params {
   int32_t horizon;       /* N (LinearMpcConfig.horizon, linear_mpc_configs.py:11) */
@@ -99,6 +101,16 @@ int mpcqp_create(const mpcqp_params* p, int32_t device, mpcqp_ctx** out);
 int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xref,
                 const float* contact, const float* feet, const float* robot, float* u0,
                 float* U, int32_t* status, int32_t* iters, void* stream /* hipStream_t */);
+
+/* Full state / input weights (mpc.py:49-52 builds kron(I_N, Q), kron(I_N, R) from any
+ * LinearMpcConfig.Q / R): Q [13][13] and R [12][12] row-major HOST arrays, symmetric and
+ * finite (else MPCQP_ERR_ARG); NULL keeps the current diagonal of that matrix.  Diagonal
+ * matrices select the diagonal fast path (equivalent to setting q_diag / r_diag).  The
+ * weights are copied before the call returns; solves issued before it are unaffected.
+ * The interior-point class (robots with more than 128 stance variables) supports a full
+ * Q and an R without cross-leg couplings (R[i][j] = 0 for legs i / 3 != j / 3); a robot of
+ * that class under weights it does not support reports MPCQP_STATUS_UNSUPPORTED. */
+int mpcqp_set_weights(mpcqp_ctx* ctx, const double* Q, const double* R);
 
 /* Largest number of stance foot-steps the caller promises per robot
  * (0 = unknown: the engine dispatches every capacity class). */

@@ -110,8 +110,10 @@ def condensed_cost(Ad, Bd, x0, xref, horizon, q_diag=Q_DIAG, r_diag=R_DIAG):
     Qbar is float64 (mpc.py:50) so H and g come out float64.
     """
     n, m, N = NUM_STATE, NUM_INPUT, horizon
-    Qbar = np.kron(np.identity(N), np.diag(q_diag))
-    Rbar = np.kron(np.identity(N), np.diag(r_diag))
+    q = np.asarray(q_diag, dtype=np.float64)   # a diagonal, or the full matrix (mpc.py:50,52)
+    r = np.asarray(r_diag, dtype=np.float64)
+    Qbar = np.kron(np.identity(N), q if q.ndim == 2 else np.diag(q))
+    Rbar = np.kron(np.identity(N), r if r.ndim == 2 else np.diag(r))
     powers = [np.identity(n, dtype=np.float32)]
     for _ in range(N):
         powers.append(powers[-1] @ Ad)
@@ -156,11 +158,12 @@ def friction_constraints(contact, horizon, mu=MU, fz_max=500.0, normal=None):
 
 
 def formulate(x0, xref, contact, feet, inertia, mass, horizon, mu=MU, fz_max=500.0,
-              dt=DT_MPC, yaw=None, normal=None):
+              dt=DT_MPC, yaw=None, normal=None, Q=Q_DIAG, R=R_DIAG):
     """The whole formulation half of mpc.py:262-275 for one robot.
 
     ``yaw`` defaults to x0[2] (mpc.py:77 stores rpy[2] both in the state and in
     self.yaw, so they agree up to the float32 rounding of the state slot).
+    ``Q`` / ``R``: diagonals or full matrices (mpc.py:50,52).
     Returns dict(H, g, C, lb, ub, Ad, Bd, Ac, Bc).
     """
     x0 = np.asarray(x0, dtype=np.float32)
@@ -168,6 +171,6 @@ def formulate(x0, xref, contact, feet, inertia, mass, horizon, mu=MU, fz_max=500
     yaw = float(x0[2]) if yaw is None else yaw
     Ac, Bc = continuous_model(yaw, np.asarray(inertia, dtype=np.float32), mass, feet)
     Ad, Bd = discretize(Ac, Bc, dt)
-    H, g, _, _ = condensed_cost(Ad, Bd, x0, xref, horizon)
+    H, g, _, _ = condensed_cost(Ad, Bd, x0, xref, horizon, Q, R)
     C, lb, ub = friction_constraints(np.asarray(contact).reshape(-1), horizon, mu, fz_max, normal)
     return dict(H=H, g=g, C=C, lb=lb, ub=ub, Ad=Ad, Bd=Bd, Ac=Ac, Bc=Bc)

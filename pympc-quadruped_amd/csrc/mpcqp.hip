@@ -25,6 +25,8 @@
 
 #include <math.h>
 #include <stdint.h>
+
+#include <cmath>
 #include <string.h>
 
 #include <new>
@@ -50,9 +52,6 @@ static_assert(kMaxN == 20, "the dense classes' and the interior-point class's LD
 #ifndef MPCQP_SWEEP_MFMA
 #define MPCQP_SWEEP_MFMA 0   // 1: class-64 H^-1 sweep blocked by 4 pivots on the f64 MFMA (parity-exact, slower: DESIGN 4.5)
 #endif
-#ifndef MPCQP_BM
-#define MPCQP_BM 0   // 1: class 64 as a brain / muscle pair of waves (mpcqp_bm.h, measured slower: DESIGN 4.5)
-#endif
 #ifndef MPCQP_C64_WPE
 #define MPCQP_C64_WPE (MPCQP_C64_TW == 4 ? 4 : 2)   // class-64 waves per SIMD (VGPR budget)
 #endif
@@ -68,6 +67,7 @@ struct KParams {
   double dt;
   double q[NX];
   double r[NU];
+  const double* wfull;   // device: full Q (13 x 13) then R (12 x 12), row-major; nullptr = diagonal q, r
 };
 
 // Diagnostic build only (-DMPCQP_STAMPS): per-phase s_memtime stamps and per-section
@@ -303,7 +303,6 @@ __device__ __forceinline__ int wave_argmin_f32(double v, double& vmin_out) {
 #include "mpcqp_form.h"
 #include "mpcqp_sweep_mfma.h"
 #include "mpcqp_solve.h"
-#include "mpcqp_bm.h"
 #include "mpcqp_ipm.h"
 #include "mpcqp_plan.h"
 
@@ -321,6 +320,7 @@ __device__ __forceinline__ int xcd_robot(int bid, int B) {
 // Class NV = 64: one 2-wave workgroup per robot of the batch.  Robots with more
 // than 64 stance variables are appended to `queue` (when given) for class 96, those
 // with more than 96 to `queue_big` (when given) for class 128.
+template <bool FULL>
 __global__ __launch_bounds__(Cfg<64>::NT) __attribute__((amdgpu_waves_per_eu(MPCQP_C64_WPE, Cfg<64>::NW))) void mpcqp_kernel_64(
     KParams P, int B, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
@@ -328,21 +328,16 @@ __global__ __launch_bounds__(Cfg<64>::NT) __attribute__((amdgpu_waves_per_eu(MPC
     int* __restrict__ queue, int* __restrict__ queue_big, int* __restrict__ queue_ipm) {
   if ((int)blockIdx.x >= B) return;
   const int b = xcd_robot(blockIdx.x, B);
-#if MPCQP_BM
-  __shared__ SharedBM sm;
-  solve_robot_bm(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, queue, queue_big,
-                 queue_ipm);
-#else
   __shared__ SharedT<64> sm;
-  solve_robot<64>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, queue, queue_big,
+  solve_robot<64, FULL>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, queue, queue_big,
                   queue_ipm);
-#endif
 }
 
 // Class NV = 96: one 6-wave workgroup (4 x 6 register tiles) per robot queued by
 // class 64 (64 < n <= 96: the N = 16 trot / pace / bound schedules); robots with more
 // stance variables go on to class 128 through `qout`.  Same launch / reset protocol
 // as class 128 below.
+template <bool FULL>
 __global__ __launch_bounds__(Cfg<96>::NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void mpcqp_kernel_96(
     KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
@@ -352,14 +347,14 @@ __global__ __launch_bounds__(Cfg<96>::NT) __attribute__((amdgpu_waves_per_eu(2, 
   const int tid = threadIdx.x;
   const int k = blockIdx.x;
   if (direct_B > 0) {   // the caller's stance range rules class 64 out: robot = workgroup
-    if (k < direct_B) solve_robot<96>(P, k, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, qout,
+    if (k < direct_B) solve_robot<96, FULL>(P, k, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, qout,
                                       nullptr, q_ipm);
     return;
   }
   const int cnt = uni(__hip_atomic_load(&queue[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (k < cnt) {
     const int b = uni(queue[4 + k]);
-    solve_robot<96>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, qout, nullptr, q_ipm);
+    solve_robot<96, FULL>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, qout, nullptr, q_ipm);
     // only the cnt workers count themselves (no contended atomic from the idle rest)
     if (tid == 0 && atomicAdd(&queue[2], 1) == cnt - 1) {
       atomicExch(&queue[0], 0);
@@ -374,6 +369,7 @@ __global__ __launch_bounds__(Cfg<96>::NT) __attribute__((amdgpu_waves_per_eu(2, 
 // workgroup to finish resets the counters for the next launch (queue[0] = count, queue[2] = finished
 // workgroups, queue[4..] = robot indices).  Workloads that fit class 64 skip this
 // launch via mpcqp_set_stance_hint.
+template <bool FULL>
 __global__ __launch_bounds__(Cfg<128>::NT) void mpcqp_kernel_128(
     KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
@@ -383,14 +379,14 @@ __global__ __launch_bounds__(Cfg<128>::NT) void mpcqp_kernel_128(
   const int tid = threadIdx.x;
   const int k = blockIdx.x;
   if (direct_B > 0) {
-    if (k < direct_B) solve_robot<128>(P, k, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg,
+    if (k < direct_B) solve_robot<128, FULL>(P, k, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg,
                                        q_ipm, nullptr, q_ipm);
     return;
   }
   const int cnt = uni(__hip_atomic_load(&queue[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (k < cnt) {
     const int b = uni(queue[4 + k]);
-    solve_robot<128>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, q_ipm, nullptr, q_ipm);
+    solve_robot<128, FULL>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, q_ipm, nullptr, q_ipm);
     // only the cnt workers count themselves (no contended atomic from the idle rest)
     if (tid == 0 && atomicAdd(&queue[2], 1) == cnt - 1) {
       atomicExch(&queue[0], 0);
@@ -462,6 +458,7 @@ struct mpcqp_ctx {
   int ncu;
   std::vector<QueueSet> queues;
   unsigned long long use_clock;
+  double* wdev;       // full Q (13 x 13) then R (12 x 12) on the device (mpcqp_set_weights); nullptr: diagonal
   double dt_control;  // planner constants (mpcqp_set_planner)
   double gravity;
   double max_pos_error;
@@ -590,6 +587,7 @@ int mpcqp_create(const mpcqp_params* p, int32_t device, mpcqp_ctx** out) {
   ctx->stance_min = 0;
   ctx->ncu = 0;
   ctx->use_clock = 0;
+  ctx->wdev = nullptr;
   ctx->dt_control = 0.001;    // linear_mpc_configs.py:6
   ctx->gravity = 9.81;        // linear_mpc_configs.py:13
   ctx->max_pos_error = 0.1;   // mpc.py:121
@@ -633,6 +631,8 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   kp.dt = ctx->params.dt;
   for (int i = 0; i < NX; ++i) kp.q[i] = ctx->params.q_diag[i];
   for (int i = 0; i < NU; ++i) kp.r[i] = ctx->params.r_diag[i];
+  kp.wfull = ctx->wdev;
+  const bool full = ctx->wdev != nullptr;   // the dense classes' full-weight instantiations
   hipStream_t st = (hipStream_t)stream;
   // A robot has n = 3 * #stance <= 12 N variables.  Robots with more than 64 are queued
   // for class 96, more than 96 for class 128, more than 128 for the interior-point
@@ -682,21 +682,21 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   hipError_t e = hipSuccess;
   int fe = MPCQP_OK;
   if (first == 0) {
-    hipLaunchKernelGGL(mpcqp_kernel_64, dim3(batch), dim3(Cfg<64>::NT), 0, st, kp, (int)batch, x0, xref, contact,
+    hipLaunchKernelGGL(full ? mpcqp_kernel_64<true> : mpcqp_kernel_64<false>, dim3(batch), dim3(Cfg<64>::NT), 0, st, kp, (int)batch, x0, xref, contact,
                        feet, robot, u0, U, (int*)status, (int*)iters, q1, q2, q3);
     e = hipGetLastError();
     if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch: ") + hipGetErrorString(e));
     if ((fe = fork_ipm()) != MPCQP_OK) return fe;
   }
   if (large && first <= 1) {
-    hipLaunchKernelGGL(mpcqp_kernel_96, dim3(batch), dim3(Cfg<96>::NT), 0, st, kp, x0, xref, contact, feet, robot,
+    hipLaunchKernelGGL(full ? mpcqp_kernel_96<true> : mpcqp_kernel_96<false>, dim3(batch), dim3(Cfg<96>::NT), 0, st, kp, x0, xref, contact, feet, robot,
                        u0, U, (int*)status, (int*)iters, q1, q2, q3, first == 1 ? (int)batch : 0);
     e = hipGetLastError();
     if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (96): ") + hipGetErrorString(e));
     if ((fe = fork_ipm()) != MPCQP_OK) return fe;
   }
   if (huge && first <= 2) {
-    hipLaunchKernelGGL(mpcqp_kernel_128, dim3(batch), dim3(Cfg<128>::NT), 0, st, kp, x0, xref, contact, feet, robot,
+    hipLaunchKernelGGL(full ? mpcqp_kernel_128<true> : mpcqp_kernel_128<false>, dim3(batch), dim3(Cfg<128>::NT), 0, st, kp, x0, xref, contact, feet, robot,
                        u0, U, (int*)status, (int*)iters, q2, q3, first == 2 ? (int)batch : 0);
     e = hipGetLastError();
     if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (128): ") + hipGetErrorString(e));
@@ -708,6 +708,64 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   } else if (fork && hipStreamWaitEvent(st, qs->ev_join, 0) != hipSuccess) {
     return set_err(ctx, MPCQP_ERR_HIP, "interior-point join failed");
   }
+  return MPCQP_OK;
+}
+
+int mpcqp_set_weights(mpcqp_ctx* ctx, const double* Q, const double* R) {
+  if (!ctx) return MPCQP_ERR_ARG;
+  double q[NX * NX], r[NU * NU];
+  for (int i = 0; i < NX * NX; ++i) q[i] = (i % (NX + 1) == 0) ? ctx->params.q_diag[i / (NX + 1)] : 0.0;
+  for (int i = 0; i < NU * NU; ++i) r[i] = (i % (NU + 1) == 0) ? ctx->params.r_diag[i / (NU + 1)] : 0.0;
+  if (Q) memcpy(q, Q, sizeof(q));
+  if (R) memcpy(r, R, sizeof(r));
+  // symmetric and finite (the reference's kron(I_N, Q) enters H = 2 Su^T Qbar Su; an
+  // asymmetric Q would make H asymmetric, which no QP solver of the reference accepts)
+  double qmax = 0.0, rmax = 0.0;
+  bool finite = true;   // per entry: fmax drops a NaN operand
+  for (int i = 0; i < NX * NX; ++i) {
+    finite = finite && std::isfinite(q[i]);
+    qmax = fmax(qmax, fabs(q[i]));
+  }
+  for (int i = 0; i < NU * NU; ++i) {
+    finite = finite && std::isfinite(r[i]);
+    rmax = fmax(rmax, fabs(r[i]));
+  }
+  if (!finite) return set_err(ctx, MPCQP_ERR_ARG, "weights: non-finite entry");
+  bool diag = true;
+  for (int i = 0; i < NX; ++i)
+    for (int j = 0; j < NX; ++j) {
+      if (fabs(q[i * NX + j] - q[j * NX + i]) > 1e-12 * qmax) return set_err(ctx, MPCQP_ERR_ARG, "weights: Q not symmetric");
+      if (i != j && q[i * NX + j] != 0.0) diag = false;
+    }
+  for (int i = 0; i < NU; ++i)
+    for (int j = 0; j < NU; ++j) {
+      if (fabs(r[i * NU + j] - r[j * NU + i]) > 1e-12 * rmax) return set_err(ctx, MPCQP_ERR_ARG, "weights: R not symmetric");
+      if (i != j && r[i * NU + j] != 0.0) diag = false;
+    }
+  for (int i = 0; i < NX; ++i) ctx->params.q_diag[i] = q[i * (NX + 1)];
+  for (int i = 0; i < NU; ++i) ctx->params.r_diag[i] = r[i * (NU + 1)];
+  DeviceScope dev(ctx->device);
+  if (!dev.ok) return set_err(ctx, MPCQP_ERR_HIP, "hipSetDevice failed");
+  if (diag) {   // the diagonal fast path (the weights live in the kernel arguments)
+    if (ctx->wdev) {
+      if (hipDeviceSynchronize() != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, "weights: device sync failed");
+      (void)hipFree(ctx->wdev);
+      ctx->wdev = nullptr;
+    }
+    return MPCQP_OK;
+  }
+  // launches on any stream (non-blocking ones included) may still read the previous weights
+  if (ctx->wdev && hipDeviceSynchronize() != hipSuccess)
+    return set_err(ctx, MPCQP_ERR_HIP, "weights: device sync failed");
+  if (!ctx->wdev && hipMalloc(&ctx->wdev, sizeof(double) * (NX * NX + NU * NU)) != hipSuccess) {
+    ctx->wdev = nullptr;
+    return set_err(ctx, MPCQP_ERR_ALLOC, "weights: allocation failed");
+  }
+  double host[NX * NX + NU * NU];
+  memcpy(host, q, sizeof(q));
+  memcpy(host + NX * NX, r, sizeof(r));
+  if (hipMemcpy(ctx->wdev, host, sizeof(host), hipMemcpyHostToDevice) != hipSuccess)
+    return set_err(ctx, MPCQP_ERR_HIP, "weights: upload failed");
   return MPCQP_OK;
 }
 
@@ -795,6 +853,7 @@ int mpcqp_destroy(mpcqp_ctx* ctx) {
     // hipFree synchronises the device before releasing the memory: no per-stream sync
     // (a recorded stream may already have been destroyed by the caller)
     for (auto& q : ctx->queues) release_set(q);
+    if (ctx->wdev) (void)hipFree(ctx->wdev);
   }
   delete ctx;
   return MPCQP_OK;

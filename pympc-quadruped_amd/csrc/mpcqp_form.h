@@ -21,6 +21,12 @@
 //     and g = 2 Su^T Qbar (Sx x0 - Xref) reduces to suffix sums over the horizon of
 //     Q e_t and t Q e_t, e_t = A^{t+1} x0 - xref_t = x0 + (t+1) n1 + C(t+1, 2) n2 - xref_t
 //     with n1 = Nm x0, n2 = Nm^2 x0 = h^2 x0[12] e_5.
+//   * full (non-diagonal) Q / R (mpc.py:49-52 builds kron(I_N, Q) from any matrix): with
+//     Y00 = X0^T Q X0, Y01 = X0^T Q X1, Y11 = X1^T Q X1 the block is
+//        2 [ m Y00 + Sb Y01 + Sa Y01^T + T Y11 ] (+ 2 R on the same-step blocks),
+//     Sa = sum_t (t - ja), Sb = sum_t (t - jb), T = sum_t (t - ja)(t - jb) over t = max..N-1
+//     (exact integers); g keeps its form with E0 / E1 = Q times the suffix sums of e_t, t e_t.
+//     The diagonal case (Y00 = Ya + Yb, Y01 = 2 Ya, Y11 = 4 Ya) keeps the two-term path.
 //   * friction cone (mpc.py:237-260): 6 one-sided rows per stance foot-step
 //     (4 pyramid rows, fz >= 0, fz <= contact * fz_max), generalised to a per-robot
 //     surface normal (normal = e_z reproduces mpc.py:239-245 exactly).
@@ -38,6 +44,11 @@ struct alignas(16) Form {
   double rz[2];                  // float32(cos yaw), float32(sin yaw)
   double minv;                   // float32(1/m)
   double q[16];                  // state weights (staged: indexed per lane below)
+  // full Q only (KParams::wfull): Q, the raw suffix sums of e_t and t e_t, X0 / X1 and Q X0 / Q X1
+  double qf[NX * NX];
+  double es[2][kMaxN][NX];
+  double X[2][NX][NU];
+  double QX[2][NX][NU];
 };
 
 // Hessian blocks {Ya, Yb}[c1][c2]: kept for the whole solve (H entries are
@@ -45,6 +56,9 @@ struct alignas(16) Form {
 struct alignas(16) FormY {
   d2 Y[NU * NU];
   double rd2[NU];   // 2 R_ii (input weights; kernel arguments indexed per lane would be memory loads)
+  // full Q / R only: Y00, Y01, Y11 and 2 R (12 x 12, row-major)
+  double Yf[3][NU * NU];
+  double rf2[NU * NU];
 };
 
 // Per-robot data every class keeps for the solve.
@@ -150,6 +164,91 @@ __device__ __forceinline__ int form_stance(const Form& f, RobotMeta& mt, int N, 
   return S;
 }
 
+// e_t's state component sc at horizon step t (0-based: e_t = A^{t+1} x0 - xref_t)
+__device__ __forceinline__ double form_e(const Form& f, int sc, int t, double h) {
+  const float* xin = f.in + IN_X0;
+  auto rz = [&](int a, int bb) -> double {
+    return a == 2 ? (bb == 2 ? 1.0 : 0.0) : (bb == 2 ? 0.0 : (a == bb ? f.rz[0] : (a == 0 ? -f.rz[1] : f.rz[1])));
+  };
+  double x0s = (double)xin[sc], n1 = 0.0, n2 = 0.0;
+  const double g12 = (double)xin[12];
+  if (sc < 3) n1 = h * (rz(0, sc) * (double)xin[6] + rz(1, sc) * (double)xin[7] + rz(2, sc) * (double)xin[8]);
+  else if (sc < 6) n1 = h * (double)xin[6 + sc] + (sc == 5 ? 0.5 * h * h * g12 : 0.0);
+  else if (sc == 11) n1 = h * g12;
+  if (sc == 5) n2 = h * h * g12;
+  const double k = (double)(t + 1);
+  return x0s + k * n1 + 0.5 * k * (k - 1.0) * n2 - (double)f.in[IN_XREF + t * NX + sc];
+}
+
+// Full (non-diagonal) Q / R (KParams::wfull): E0 / E1 = Q times the suffix sums of e_t and
+// t e_t, and the closed-form blocks Y00 = X0^T Q X0, Y01 = X0^T Q X1, Y11 = X1^T Q X1 with X0
+// = B_d, X1 = Nm B_d written out (K, G, minv are in LDS: called after their barrier).
+template <int NT>
+__device__ __forceinline__ void form_model_full(const KParams& P, Form& f, FormY& fy, int N, int tid) {
+  const double h = P.dt;
+  fsync<NT>();   // K, G (written just before by threads < 36) are read below
+  for (int e = tid; e < NX * NX; e += NT) f.qf[e] = P.wfull[e];
+  for (int e = tid; e < NU * NU; e += NT) fy.rf2[e] = 2.0 * P.wfull[NX * NX + e];
+  // X0 (rows: G h^2/2, S h^2/(2m), K h, S h/m, 0) and X1 = Nm X0 (G h^2, S h^2/m, 0, 0, 0)
+  for (int e = tid; e < NX * NU; e += NT) {
+    const int i = e / NU, c = e % NU;
+    double x0v = 0.0, x1v = 0.0;
+    if (i < 3) {
+      x0v = f.G[i][c] * (0.5 * h * h);
+      x1v = f.G[i][c] * (h * h);
+    } else if (i < 6) {
+      const double on = (c % 3 == i - 3) ? f.minv : 0.0;
+      x0v = on * (0.5 * h * h);
+      x1v = on * (h * h);
+    } else if (i < 9) {
+      x0v = f.K[i - 6][c] * h;
+    } else if (i < 12) {
+      x0v = (c % 3 == i - 9) ? f.minv * h : 0.0;
+    }
+    f.X[0][i][c] = x0v;
+    f.X[1][i][c] = x1v;
+  }
+  // raw suffix sums of e_t and t e_t, thread = state component
+  if (tid < NX) {
+    double s0 = 0.0, s1 = 0.0;
+    for (int t = N - 1; t >= 0; --t) {
+      const double e = form_e(f, tid, t, h);
+      s0 += e;
+      s1 = fma((double)t, e, s1);
+      f.es[0][t][tid] = s0;
+      f.es[1][t][tid] = s1;
+    }
+  }
+  fsync<NT>();
+  for (int e = tid; e < 2 * NX * NU; e += NT) {   // Q X0, Q X1
+    const int w = e / (NX * NU), i = (e / NU) % NX, c = e % NU;
+    double a = 0.0;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) a = fma(f.qf[i * NX + j], f.X[w][j][c], a);
+    f.QX[w][i][c] = a;
+  }
+  for (int e = tid; e < N * NX; e += NT) {   // E0 = Q es0, E1 = Q es1 (components < 6)
+    const int t = e / NX, sc = e % NX;
+    double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      a0 = fma(f.qf[sc * NX + j], f.es[0][t][j], a0);
+      a1 = fma(f.qf[sc * NX + j], f.es[1][t][j], a1);
+    }
+    f.E0[t][sc] = a0;
+    if (sc < 6) f.E1[t][sc] = a1;
+  }
+  fsync<NT>();
+  for (int e = tid; e < 3 * NU * NU; e += NT) {   // Y00 = X0^T Q X0, Y01 = X0^T Q X1, Y11 = X1^T Q X1
+    const int w = e / (NU * NU), c1 = (e / NU) % NU, c2 = e % NU;
+    const int xa = w == 2 ? 1 : 0, qb = w == 0 ? 0 : 1;
+    double a = 0.0;
+#pragma unroll
+    for (int i = 0; i < NX; ++i) a = fma(f.X[xa][i][c1], f.QX[qb][i][c2], a);
+    fy.Yf[w][c1 * NU + c2] = a;
+  }
+}
+
 // Model (float32-faithful), cone rows, Ya/Yb, horizon suffix sums.  All NT threads.
 template <int NT>
 __device__ __forceinline__ void form_model(const KParams& P, Form& f, FormY& fy, RobotMeta& mt, int N, int tid) {
@@ -236,6 +335,10 @@ __device__ __forceinline__ void form_model(const KParams& P, Form& f, FormY& fy,
   }
   // ---- horizon suffix sums of Q e_t and t Q e_t; thread s (state component)
   if (tid < NU) fy.rd2[tid] = 2.0 * P.r[tid];
+  if (P.wfull) {
+    form_model_full<NT>(P, f, fy, N, tid);
+    return;
+  }
   if (tid >= 64 - 16 && tid < 64 - 16 + NX) {
     const int sc = tid - (64 - 16);
     const float* xin = f.in + IN_X0;
@@ -290,6 +393,21 @@ __device__ __forceinline__ double form_g(const KParams& P, const Form& f, const 
   const double al1 = f.G[0][cc] * E1[0] + f.G[1][cc] * E1[1] + f.G[2][cc] * E1[2] + E1[3 + ax] * f.minv;
   const double be0 = f.K[0][cc] * E0[6] + f.K[1][cc] * E0[7] + f.K[2][cc] * E0[8] + E0[9 + ax] * f.minv;
   return 2.0 * (0.5 * h * h * ((double)(1 - 2 * j) * al0 + 2.0 * al1) + h * be0);
+}
+
+// H[a][b] for full Q / R (header comment), the same-step R block included
+__device__ __forceinline__ double form_h_full(const FormY& fy, int N, int ja, int ca, int jb, int cb) {
+  const int mx = ja > jb ? ja : jb;
+  const int m = N - mx, da = mx - ja, db = mx - jb;   // N <= 20: every product fits an int
+  const int s1 = (m * (m - 1)) >> 1;
+  const double sa = (double)(s1 + m * da), sb = (double)(s1 + m * db);
+  const double tt = (double)(((m - 1) * m * (2 * m - 1)) / 6 + (da + db) * s1 + m * da * db);
+  double v = (double)m * fy.Yf[0][ca * NU + cb];
+  v = fma(sb, fy.Yf[1][ca * NU + cb], v);
+  v = fma(sa, fy.Yf[1][cb * NU + ca], v);
+  v = fma(tt, fy.Yf[2][ca * NU + cb], v);
+  const double rv = fy.rf2[ca * NU + cb];   // unconditional: a guarded load splits the block
+  return fma(2.0, v, ja == jb ? rv : 0.0);
 }
 
 // H[a][b] from the foot-steps' horizon steps (ja, jb) and input columns (ca, cb)

@@ -64,6 +64,8 @@ struct alignas(16) IpmShared {
   double xr[kMaxN][NX];            // xref, float64
   double qh[16];                   // 2 q
   double rh[NU];                   // 2 r
+  double qf[NX][NX];               // Qh = 2 Q (full; the diagonal case fills the diagonal)
+  double rf[NU][NU];               // Rh = 2 R (leg blocks used)
   double W[IPM_NF][9];             // per stance foot-step 3x3 weight of the Newton system
   alignas(16) double P[144];       // P_{k+1}
   alignas(16) double U[kMaxN][NU]; // iterate (swing entries 0)
@@ -158,6 +160,15 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     write_empty_t<NT>(b, lane, N, MPCQP_STATUS_OK, u0g, Ug, statusg, itersg);
     return;
   }
+  if (KP.wfull) {   // full weights: cross-leg R couplings break the per-foot-step weights
+    bool cross = false;
+    for (int e = lane; e < NU * NU; e += NT)
+      cross |= (e / NU) / 3 != (e % NU) / 3 && KP.wfull[NX * NX + e] != 0.0;
+    if (__any(cross)) {
+      write_empty_t<NT>(b, lane, N, MPCQP_STATUS_UNSUPPORTED, u0g, Ug, statusg, itersg);
+      return;
+    }
+  }
   form_model<NT>(KP, smf, sm.fa.fy, sm.mt, N, lane);
   fsync<NT>();
   {
@@ -183,6 +194,14 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       sm.qh[lane] = 2.0 * KP.q[lane];
     }
     if (lane < NU) sm.rh[lane] = 2.0 * KP.r[lane];
+    for (int e = lane; e < NX * NX; e += NT) {
+      const int i = e / NX, j = e % NX;
+      sm.qf[i][j] = KP.wfull ? 2.0 * KP.wfull[e] : (i == j ? 2.0 * KP.q[i] : 0.0);
+    }
+    for (int e = lane; e < NU * NU; e += NT) {
+      const int i = e / NU, j = e % NU;
+      sm.rf[i][j] = KP.wfull ? 2.0 * KP.wfull[NX * NX + e] : (i == j ? 2.0 * KP.r[i] : 0.0);
+    }
     for (int e = lane; e < N * NX; e += NT) sm.xr[e / NX][e % NX] = (double)smf.in[IN_XREF + e];
     for (int e = lane; e < N * NU; e += NT) sm.U[e / NU][e % NU] = 0.0;
   }
@@ -207,11 +226,12 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     o[2] = p[2];
   };
   auto foot_ptr = [&](int j, double (*A)[NU]) -> double* { return &A[sm.mt.foot_t[j]][3 * sm.mt.foot_leg[j]]; };
-  auto legrh = [&](int j, double (&o)[3]) {
+  auto legrh = [&](int j, double (&o)[9]) {   // the leg's 3 x 3 block of Rh
     const int l = sm.mt.foot_leg[j];
-    o[0] = sm.rh[3 * l];
-    o[1] = sm.rh[3 * l + 1];
-    o[2] = sm.rh[3 * l + 2];
+#pragma unroll
+    for (int x = 0; x < 3; ++x)
+#pragma unroll
+      for (int y = 0; y < 3; ++y) o[3 * x + y] = sm.rf[3 * l + x][3 * l + y];
   };
 
 #ifdef MPCQP_IPM_DEBUG
@@ -292,7 +312,11 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     double nu = 0.0;
     const int li = lane < NX ? lane : 0;
     for (int k = N - 1; k >= 0; --k) {
-      double v = lane < NX ? sm.qh[li] * (sm.X[k + 1][li] - sm.xr[k][li]) : 0.0;
+      double v = 0.0;
+      if (lane < NX) {
+#pragma unroll
+        for (int j = 0; j < NX; ++j) v = fma(sm.qf[li][j], sm.X[k + 1][j] - sm.xr[k][j], v);
+      }
       if (k < N - 1) {
         double s[7];
 #pragma unroll
@@ -309,7 +333,10 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       double bcl[12], nv[12];
       ld12(bcl, sm.BmT[c]);
       ld12(nv, sm.nuh[k]);
-      const double g = sm.rh[c] * sm.U[k][c] + dot12(bcl, nv);
+      const int c3 = 3 * (c / 3);   // Rh's leg block (no cross-leg couplings in this class)
+      const double ru = fma(sm.rf[c][c3 + 2], sm.U[k][c3 + 2],
+                            fma(sm.rf[c][c3 + 1], sm.U[k][c3 + 1], sm.rf[c][c3] * sm.U[k][c3]));
+      const double g = ru + dot12(bcl, nv);
       sm.gr[k][c] = sm.mt.stance_of[4 * k + c / 3] >= 0 ? g : 0.0;
     }
     fsync<NT>();
@@ -349,6 +376,12 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
 #pragma unroll
     for (int a2 = 0; a2 < 3; ++a2) bx[q][a2] = ok ? sm.Bm[lcc][3 * (cc / 3) + a2] : 0.0;
   }
+  auto qhat4 = [&]() -> d4 {   // Qh's 12 x 12 moving-state block in result layout
+    d4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = (lr + 4 * i < 12 && lc < 12) ? sm.qf[lr + 4 * i][lc] : 0.0;
+    return v;
+  };
   auto diag4 = [&](double d) -> d4 {   // d I (12 x 12) in result layout
     d4 v;
 #pragma unroll
@@ -389,7 +422,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
 
   auto factor = [&]() {
     IPM_T0();
-    d4 Pr = diag4(sm.qh[lcc]);
+    d4 Pr = qhat4();
     d4 Er = stage_e(N - 1), Sp = diag4(0.0), Ep = diag4(0.0);
     const int jc = lane < 12 ? lane : (lane < 24 ? lane - 12 : 0);
     for (int k = N - 1; k >= 0; --k) {
@@ -445,7 +478,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
         d4 SA = Sr;
 #pragma unroll
         for (int q = 0; q < 2; ++q) SA = mfma(Sr[q], Nmb[q], SA);
-        Pr = diag4(sm.qh[lcc]);
+        Pr = qhat4();
 #pragma unroll
         for (int i = 0; i < 4; ++i) Pr[i] += SA[i];
 #pragma unroll
@@ -630,7 +663,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
 
   // ---- start: minimiser under a mild barrier weight, slacks shifted into the interior
   for (int j = lane; j < S; j += NT) {
-    double d[6], rh[3], wv[9];
+    double d[6], rh[9], wv[9];
 #pragma unroll
     for (int r = 0; r < 6; ++r) d[r] = 1e-2;
     legrh(j, rh);
@@ -661,7 +694,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
   // ---- active-set polish on the rows sm.fact; true when verified (sm.U = the optimum)
   auto polish = [&]() -> bool {
     for (int j = lane; j < S; j += NT) {
-      double rh[3], pj[9], fp[3], wv[9];
+      double rh[9], pj[9], fp[3], wv[9];
       legrh(j, rh);
       ipm_foot_nullspace(rw, sm.fact[j] & liv, -sm.mt.ub[j], rh, pj, fp, wv);
 #pragma unroll
@@ -723,7 +756,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       double best = INFINITY;
       int drop = -1;
       if (am) {
-        double pjl[9], fpd[3], wd[9], rh[3];
+        double pjl[9], fpd[3], wd[9], rh[9];
         legrh(j, rh);
         const int nq = ipm_foot_nullspace(rw, am, h5, rh, pjl, fpd, wd);
         ipm_cone_multipliers(rw, am, nq, g, tol_g, best, drop);
@@ -809,7 +842,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       fsync<NT>();
     }
     for (int j = lane; j < S; j += NT) {
-      double d[6], rh[3], wv[9];
+      double d[6], rh[9], wv[9];
 #pragma unroll
       for (int r = 0; r < 6; ++r) d[r] = ((liv >> r) & 1) ? sm.fl[j][r] / sm.fs[j][r] : 0.0;
       legrh(j, rh);

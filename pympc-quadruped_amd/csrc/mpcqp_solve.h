@@ -173,7 +173,7 @@ __device__ __forceinline__ void write_empty_t(int b, int tid, int N, int code, f
 // One robot.  A robot exceeding NV is appended to `queue` (when given) for the
 // next capacity class -- or to `queue_big` / `queue_ipm` for the ones after, when
 // it exceeds those too -- otherwise reported MPCQP_STATUS_TOO_LARGE.
-template <int NV>
+template <int NV, bool FULL>
 __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>& sm, const float* __restrict__ x0g,
                                             const float* __restrict__ xrefg, const float* __restrict__ contactg,
                                             const float* __restrict__ feetg, const float* __restrict__ robotg,
@@ -236,6 +236,8 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       cc[c] = 3 * sm.mt.foot_leg[sb] + col % 3;
     }
   };
+  // FULL: non-diagonal Q / R (form_h_full, the same-step R block included); the kernels
+  // are instantiated once per weight kind, so each keeps a single register assignment
   auto hrow = [&](int r, const int (&cj)[TW], const int (&cc)[TW], double (&h)[TW]) {
     const int row = 4 * tr + r;
     const int sa = row < n ? row / 3 : 0;
@@ -245,7 +247,9 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
     for (int c = 0; c < TW; ++c) {
       const int col = TW * tc + c;
-      const double hv = form_h(smfy, N, ja, car, cj[c], cc[c]) + (row == col ? r2 : 0.0);
+      double hv;
+      if constexpr (FULL) hv = form_h_full(smfy, N, ja, car, cj[c], cc[c]);
+      else hv = form_h(smfy, N, ja, car, cj[c], cc[c]) + (row == col ? r2 : 0.0);
       h[c] = (row < n && col < n) ? hv : (row == col ? 1.0 : 0.0);
     }
   };
@@ -1025,3 +1029,4 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     }
   }
 }
+

@@ -22,8 +22,9 @@ Behaviour kept from the reference:
   * an unsuccessful solve (iteration cap) still returns the best iterate
     (mpc.py:284-286 never checks is_success), with a warning; non-finite inputs
     raise (there is no iterate to return);
-  * Q and R must be diagonal (the reference's are, linear_mpc_configs.py:19-20);
-    a weight with off-diagonal entries raises instead of being truncated.
+  * Q and R are taken whole (mpc.py:50,52): full symmetric matrices go to the
+    engine's general-weight path (mpcqp_set_weights), diagonal ones to its
+    diagonal fast path; an asymmetric weight raises.
 """
 import math
 import os
@@ -48,20 +49,17 @@ def quat2ZYXangle(quat):
     return [roll, pitch, yaw]
 
 
-def _diagonal_weights(W, n, name):
-    """The diagonal of LinearMpcConfig.Q / .R (mpc.py:50,52 build Qbar = kron(I_N, Q)).
-    The engine's closed-form condensing needs a diagonal weight: a matrix with
-    off-diagonal entries is rejected rather than silently truncated."""
+def _weight_matrix(W, n, name):
+    """LinearMpcConfig.Q / .R as an n x n float64 matrix (mpc.py:50,52 build Qbar =
+    kron(I_N, Q)); a length-n vector is read as the diagonal."""
     W = np.asarray(W, dtype=np.float64)
-    if W.ndim == 1 and W.shape == (n,):
-        return W.copy()
+    if W.shape == (n,):
+        return np.diag(W)
     if W.shape != (n, n):
         raise ValueError(f"{name} must be {n}x{n} (or its diagonal), got {W.shape}")
-    off = W - np.diag(np.diag(W))
-    if np.any(off != 0.0):
-        raise ValueError(f"{name} has off-diagonal entries; the engine supports diagonal weights "
-                         f"only (the reference configs are diagonal, linear_mpc_configs.py:19-20)")
-    return np.diag(W).copy()
+    if np.any(np.abs(W - W.T) > 1e-12 * max(float(np.abs(W).max()), 1e-300)):
+        raise ValueError(f"{name} is not symmetric")
+    return W.copy()
 
 
 class ModelPredictiveController():
@@ -75,7 +73,7 @@ class ModelPredictiveController():
         self._engine = None
 
     def _load_parameters(self, mpc_config, robot_config):
-        """mpc.py:35-52 (Qbar/Rbar become the engine's diagonal weights)."""
+        """mpc.py:35-52 (Qbar / Rbar become the engine's weights)."""
         self.dt_control = mpc_config.dt_control
         self.iterations_between_mpc = mpc_config.iteration_between_mpc
         self.dt = 0.05
@@ -90,8 +88,8 @@ class ModelPredictiveController():
         self.base_inertia_base = robot_config.base_inertia_base
         self.mass = robot_config.mass_base
         self.com_height_des = robot_config.base_height_des
-        self.q_diag = _diagonal_weights(mpc_config.Q, 13, "Q")
-        self.r_diag = _diagonal_weights(mpc_config.R, 12, "R")
+        self.Q = _weight_matrix(mpc_config.Q, 13, "Q")
+        self.R = _weight_matrix(mpc_config.R, 12, "R")
         I = np.asarray(self.base_inertia_base, dtype=np.float32)
         self._robot_record = pack_robot(
             dict(mass=float(self.mass), fz_max=float(self.fz_max), mu=float(self.mu),
@@ -104,7 +102,7 @@ class ModelPredictiveController():
             from mpcqp import LinearMpc
             from mpcqp._lib import PLAN_STRIDE
             e = LinearMpc(horizon=self.horizon, robot=self._robot_record, dt=self.dt,
-                          Q=self.q_diag, R=self.r_diag, device=os.environ.get("MPCQP_DEVICE", "cuda:0"))
+                          Q=self.Q, R=self.R, device=os.environ.get("MPCQP_DEVICE", "cuda:0"))
             e.set_planner(dt_control=self.dt_control, gravity=self.gravity)
             d, f32 = e.device, dict(dtype=torch.float32, device=e.device)
             N = self.horizon

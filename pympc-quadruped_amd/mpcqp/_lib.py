@@ -12,11 +12,15 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MPCQP_LIB") or os.path.join(_HERE, "libmpcqp.so")
 
 MPCQP_OK = 0
+ERR_ARG = -1
+ERR_HIP = -2
+ERR_ALLOC = -3
 STATUS_OK = 0
 STATUS_MAX_ITER = 1
 STATUS_INFEASIBLE = 2
 STATUS_TOO_LARGE = 3
 STATUS_NONFINITE = 4
+STATUS_UNSUPPORTED = 5
 ROBOT_STRIDE = 16
 MAX_HORIZON = 20    # MPCQP_MAX_HORIZON: mpcqp_create rejects a longer horizon
 
@@ -28,6 +32,7 @@ EXPORTED_SYMBOLS = (
     "mpcqp_solve",
     "mpcqp_set_stance_hint",
     "mpcqp_set_stance_range",
+    "mpcqp_set_weights",
     "mpcqp_destroy",
     "mpcqp_last_error",
     "mpcqp_plan",
@@ -35,7 +40,7 @@ EXPORTED_SYMBOLS = (
     "mpcqp_set_planner",
     "mpcqp_stance_torques",
 )
-ABI_VERSION = 3
+ABI_VERSION = 4
 PLAN_STRIDE = 8     # MPCQP_PLAN_STRIDE: float64 planner state per robot
 GAIT_STRIDE = 9     # MPCQP_GAIT_STRIDE: period, offsets[4], durations[4]
 PLAN_REFERENCE = 1      # MPCQP_PLAN_REFERENCE: build X_ref (+ gait table) this tick
@@ -82,6 +87,8 @@ def load():
     lib.mpcqp_set_stance_hint.argtypes = [vp, i32]
     lib.mpcqp_set_stance_range.restype = ctypes.c_int
     lib.mpcqp_set_stance_range.argtypes = [vp, i32, i32]
+    lib.mpcqp_set_weights.restype = ctypes.c_int
+    lib.mpcqp_set_weights.argtypes = [vp, vp, vp]
     lib.mpcqp_destroy.restype = ctypes.c_int
     lib.mpcqp_destroy.argtypes = [vp]
     lib.mpcqp_last_error.restype = ctypes.c_char_p

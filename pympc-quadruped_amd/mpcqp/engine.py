@@ -19,16 +19,19 @@ from . import _lib
 from .params import (DT_MPC, Q_DIAG, R_DIAG, ROBOT_PRESETS, ROBOT_STRIDE, pack_robot)
 
 
-def _diag(W, n, name):
-    """Diagonal weights from a length-n vector or an n x n diagonal matrix; off-diagonal
-    entries raise (the closed-form condensing assumes diagonal Q / R, mpc.py:50,52)."""
+def _weights(W, n, name):
+    """(diagonal, full) from a length-n vector or an n x n matrix: ``full`` is the
+    row-major float64 matrix when it has off-diagonal entries (mpcqp_set_weights),
+    else None (the diagonal fast path; mpc.py:50,52 build Qbar / Rbar by kron)."""
     W = np.asarray(W, dtype=np.float64)
     if W.shape == (n,):
-        return W
+        return W, None
     if W.shape == (n, n):
         if np.any(W - np.diag(np.diag(W)) != 0.0):
-            raise ValueError(f"{name} has off-diagonal entries: only diagonal weights are supported")
-        return np.diag(W)
+            if not np.allclose(W, W.T, rtol=0.0, atol=1e-12 * max(np.abs(W).max(), 1e-300)):
+                raise ValueError(f"{name} is not symmetric")
+            return np.diag(W).copy(), np.ascontiguousarray(W)
+        return np.diag(W).copy(), None
     raise ValueError(f"{name}: expected ({n},) or ({n}, {n}), got {W.shape}")
 
 
@@ -51,7 +54,8 @@ class LinearMpc:
       robot:    default per-robot parameters: a preset name ("a1", "aliengo"),
                 a reference RobotConfig class, or a packed [16] record.
       dt:       model step (hard-coded 0.05 in mpc.py:38)
-      Q, R:     diagonal weights (linear_mpc_configs.py:19-20)
+      Q, R:     weights (linear_mpc_configs.py:19-20): [13] / [12] diagonals or full
+                symmetric 13 x 13 / 12 x 12 matrices (set_weights)
       device:   torch device of the HIP context (default cuda:0)
       max_iter: active-set iteration cap per robot (0 = engine default)
       max_stance: optional promise of at most this many stance foot-steps per
@@ -71,9 +75,11 @@ class LinearMpc:
         p = _lib.default_params(self.horizon)
         p.dt = float(dt)
         p.max_iter = int(max_iter)
-        for i, v in enumerate(_diag(Q, 13, "Q")):
+        qd, qf = _weights(Q, 13, "Q")
+        rd, rf = _weights(R, 12, "R")
+        for i, v in enumerate(qd):
             p.q_diag[i] = float(v)
-        for i, v in enumerate(_diag(R, 12, "R")):
+        for i, v in enumerate(rd):
             p.r_diag[i] = float(v)
         self.params = p
         ctx = ctypes.c_void_p()
@@ -81,10 +87,24 @@ class LinearMpc:
         _lib.check(None, self.lib.mpcqp_create(ctypes.byref(p), int(idx), ctypes.byref(ctx)),
                    "mpcqp_create")
         self._ctx = ctx
+        if qf is not None or rf is not None:
+            self.set_weights(Q, R)
         self._hint = (0, 0)
         if max_stance:
             self.set_stance_hint(max_stance)
         self.default_robot = self._robot_record(robot)
+
+    def set_weights(self, Q, R):
+        """Replace the cost weights (include/mpcqp.h mpcqp_set_weights): diagonals or full
+        symmetric matrices.  A cross-leg R entry is not supported by the interior-point
+        class (n > 128 variables): those robots return MPCQP_STATUS_UNSUPPORTED."""
+        qd, qf = _weights(Q, 13, "Q")
+        rd, rf = _weights(R, 12, "R")
+        qm = np.ascontiguousarray(qf if qf is not None else np.diag(qd), dtype=np.float64)
+        rm = np.ascontiguousarray(rf if rf is not None else np.diag(rd), dtype=np.float64)
+        _lib.check(self._ctx, self.lib.mpcqp_set_weights(self._ctx, qm.ctypes.data, rm.ctypes.data),
+                   "mpcqp_set_weights")
+        self.weights = (qm, rm)
 
     def set_stance_hint(self, max_stance):
         """Promise at most ``max_stance`` stance foot-steps per robot in the following

@@ -2,11 +2,12 @@
 import numpy as np
 
 from oracle import formulation as F
-from oracle import qp as Q
+from oracle import qp as QP
 
 
-def oracle_solution(batch, b, horizon):
-    """Reference-faithful formulation + exact QP optimum for robot b of a batch."""
+def oracle_solution(batch, b, horizon, Q=F.Q_DIAG, R=F.R_DIAG):
+    """Reference-faithful formulation + exact QP optimum for robot b of a batch
+    (``Q`` / ``R``: diagonals or full matrices, mpc.py:50,52)."""
     x0 = batch["x0"][b]
     xref = batch["xref"][b].reshape(-1)
     contact = batch["contact"][b].reshape(-1)
@@ -16,8 +17,8 @@ def oracle_solution(batch, b, horizon):
                         [rec[3], rec[5], rec[6]]], dtype=np.float32)
     normal = rec[9:12].astype(np.float64)
     o = F.formulate(x0, xref, contact, feet, inertia, float(rec[0]), horizon,
-                    mu=float(rec[7]), fz_max=float(rec[8]), normal=normal)
-    x, y, info = Q.solve_qp_dual_active_set(o["H"], o["g"], o["C"], o["lb"], o["ub"])
+                    mu=float(rec[7]), fz_max=float(rec[8]), normal=normal, Q=Q, R=R)
+    x, y, info = QP.solve_qp_dual_active_set(o["H"], o["g"], o["C"], o["lb"], o["ub"])
     return x, o, info
 
 

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     lib = _lib.load()
     for name in _declared():
         assert hasattr(lib, name), name
-    assert lib.mpcqp_abi_version() == _lib.ABI_VERSION == 3
+    assert lib.mpcqp_abi_version() == _lib.ABI_VERSION == 4
 
 
 def test_params_struct_layout():

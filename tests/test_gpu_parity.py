@@ -341,3 +341,107 @@ def test_stance_range_rejects_impossible_minimum_and_empty_ipm_robot():
     for b in (0, 2):
         x, _, _ = oracle_solution(bt, b, N)
         assert rel_err_u0(u0[b], x[:12]) < TOL_U0, b
+
+
+def _full_weights(seed, cross_leg_r=False):
+    """A symmetric positive-semidefinite Q coupling the state components (the reference's
+    diagonal scaled by a correlation matrix, |rho| <= 0.4: the weighting keeps the
+    reference's scale, so the float32 condensing of mpc.py:213-230 perturbs the optimum
+    as little as with the diagonal) and a leg-block R (or one with cross-leg terms)."""
+    from mpcqp.params import Q_DIAG, R_DIAG
+    rng = np.random.default_rng(seed)
+    C = np.eye(13)
+    for _ in range(12):
+        i, j = rng.choice(12, size=2, replace=False)   # state 12 (gravity) keeps weight 0
+        C[i, j] = C[j, i] = rng.uniform(-0.4, 0.4)
+    w, V = np.linalg.eigh(C)
+    C = V @ np.diag(np.maximum(w, 0.05)) @ V.T           # positive definite
+    d = np.sqrt(np.diag(C))
+    C = C / np.outer(d, d)
+    sq = np.sqrt(np.asarray(Q_DIAG, np.float64))
+    Q = np.outer(sq, sq) * C
+    R = np.diag(R_DIAG).copy()
+    for leg in range(4):
+        S = rng.uniform(-0.3, 0.3, size=(3, 3))
+        R[3 * leg:3 * leg + 3, 3 * leg:3 * leg + 3] += 1e-5 * (S @ S.T)
+    if cross_leg_r:
+        R[1, 7] = R[7, 1] = 3e-6
+    return 0.5 * (Q + Q.T), 0.5 * (R + R.T)
+
+
+@pytest.mark.parametrize("N", [10, 16, 20])
+def test_full_weights_match_oracle(N):
+    """General (non-diagonal) Q and leg-block R (mpc.py:50,52 take full matrices,
+    mpcqp_set_weights): random contact patterns route robots to every dense class and,
+    at N = 16 / 20, the interior-point class -- u0 and U against the float64 oracle
+    formulated with the same full Qbar = kron(I_N, Q), Rbar = kron(I_N, R)."""
+    from mpcqp.synthetic import make_batch
+    B = 24
+    rng = np.random.default_rng(300 + N)
+    bt = make_batch(B, N, seed=400 + N, gaits=("trot10", "pace10", "bound8"), robots=("a1", "aliengo"),
+                    tilt_deg=15.0)
+    density = rng.uniform(0.05, 1.0, size=(B, 1, 1))
+    bt["contact"] = (rng.random((B, N, 4)) < density).astype(np.float32)
+    bt["contact"][0] = 1.0
+    Q, R = _full_weights(N)
+    eng = _engine(N, Q=Q, R=R)
+    u0, U, status, _ = _solve(eng, bt)
+    assert (status == 0).all(), status
+    stance = bt["contact"].reshape(B, -1).sum(1)
+    worst, worst_ipm = 0.0, 0.0
+    for b in range(B):
+        x, _, _ = oracle_solution(bt, b, N, Q=Q, R=R)
+        e = max(rel_err_u0(u0[b], x[:12]), rel_err_u0(U[b], x))
+        assert e < TOL_U0, (b, int(stance[b]), e)
+        if 3 * stance[b] > 128:
+            worst_ipm = max(worst_ipm, e)
+        else:
+            worst = max(worst, e)
+    assert worst < TOL_ACHIEVED, worst
+    assert worst_ipm < TOL_ACHIEVED_IPM, worst_ipm
+    # back to the diagonal weights: the fast path again, bitwise as a fresh engine
+    from mpcqp.params import Q_DIAG, R_DIAG
+    eng.set_weights(Q_DIAG, R_DIAG)
+    got = _solve(eng, bt)
+    ref = _solve(_engine(N), bt)
+    for a, c in zip(got, ref):
+        np.testing.assert_array_equal(a, c)
+
+
+def test_full_weights_cross_leg_r_and_validation():
+    """A cross-leg R entry: the dense classes solve it (oracle parity); the
+    interior-point class, whose Riccati stages are per leg, reports
+    MPCQP_STATUS_UNSUPPORTED for its robots.  The C ABI rejects an asymmetric or
+    non-finite weight with MPCQP_ERR_ARG and keeps the previous weights."""
+    import ctypes
+    from mpcqp import _lib
+    from mpcqp.synthetic import make_batch
+    N = 16
+    B = 8
+    bt = make_batch(B, N, seed=77, gaits=("trot10",), robots=("a1",))
+    bt["contact"][::4] = 1.0   # robots 0, 4 standing: n = 192, the interior-point class
+    Q, R = _full_weights(5, cross_leg_r=True)
+    eng = _engine(N, Q=Q, R=R)
+    u0, U, status, _ = _solve(eng, bt)
+    for b in range(B):
+        if b % 4 == 0:
+            assert status[b] == _lib.STATUS_UNSUPPORTED, status
+            continue
+        assert status[b] == 0, status
+        x, _, _ = oracle_solution(bt, b, N, Q=Q, R=R)
+        assert max(rel_err_u0(u0[b], x[:12]), rel_err_u0(U[b], x)) < TOL_ACHIEVED, b
+    def set_raw(ctx, q, r):
+        return int(eng.lib.mpcqp_set_weights(ctx, np.ascontiguousarray(q).ctypes.data,
+                                             np.ascontiguousarray(r).ctypes.data))
+    bad = Q.copy()
+    bad[0, 1] += 1.0
+    assert set_raw(eng._ctx, bad, R) == _lib.ERR_ARG
+    nan = Q.copy()
+    nan[3, 3] = np.nan
+    assert set_raw(eng._ctx, nan, R) == _lib.ERR_ARG
+    inf = R.copy()
+    inf[2, 2] = np.inf
+    assert set_raw(eng._ctx, Q, inf) == _lib.ERR_ARG
+    assert set_raw(ctypes.c_void_p(0), Q, R) == _lib.ERR_ARG
+    again = _solve(eng, bt)   # the previous (valid) weights still in force
+    np.testing.assert_array_equal(again[0], u0)

@@ -152,25 +152,44 @@ def test_shim_run_ahead_uploads_keep_every_tick():
     np.testing.assert_allclose(st[:3], [o.xpos_des, o.ypos_des, o.yaw_des], rtol=0, atol=1e-7)
 
 
-def test_shim_rejects_non_diagonal_weights():
-    """mpc.py:50,52 build Qbar = kron(I_N, Q) from a full matrix; the engine's closed
-    form needs a diagonal Q / R, so an off-diagonal entry raises (never truncated)."""
+def test_shim_takes_full_weights():
+    """mpc.py:50,52 build Qbar = kron(I_N, Q) from full matrices: the shim keeps Q / R
+    whole (the engine's general-weight path, mpcqp_set_weights); asymmetric raises."""
     m = _shim()
 
     class OffDiagQ(LinearMpcConfig):
         Q = LinearMpcConfig.Q.copy()
     OffDiagQ.Q[0, 1] = OffDiagQ.Q[1, 0] = 0.5
 
-    class OffDiagR(LinearMpcConfig):
+    class AsymR(LinearMpcConfig):
         R = LinearMpcConfig.R.copy()
-    OffDiagR.R[3, 4] = 1e-6
+    AsymR.R[3, 4] = 1e-6
 
-    with pytest.raises(ValueError, match="off-diagonal"):
-        m.ModelPredictiveController(OffDiagQ, AliengoConfig)
-    with pytest.raises(ValueError, match="off-diagonal"):
-        m.ModelPredictiveController(OffDiagR, AliengoConfig)
-    c = m.ModelPredictiveController(LinearMpcConfig, AliengoConfig)   # diagonal: accepted
-    np.testing.assert_array_equal(c.q_diag, np.diag(LinearMpcConfig.Q))
+    c = m.ModelPredictiveController(OffDiagQ, AliengoConfig)
+    np.testing.assert_array_equal(c.Q, OffDiagQ.Q)
+    with pytest.raises(ValueError, match="not symmetric"):
+        m.ModelPredictiveController(AsymR, AliengoConfig)
+    c = m.ModelPredictiveController(LinearMpcConfig, AliengoConfig)
+    np.testing.assert_array_equal(c.Q, LinearMpcConfig.Q)
+    np.testing.assert_array_equal(c.R, LinearMpcConfig.R)
+
+
+def test_engine_weight_split():
+    """engine._weights: diagonal input keeps the fast path (full is None); a symmetric
+    off-diagonal matrix is passed whole; an asymmetric one raises."""
+    _shim()   # puts the package on sys.path
+    from mpcqp.engine import _weights
+    d, f = _weights(np.arange(13.0), 13, "Q")
+    assert f is None and d.shape == (13,)
+    d, f = _weights(np.diag(np.arange(12.0)), 12, "R")
+    assert f is None and list(d) == list(range(12))
+    W = np.diag(np.arange(1.0, 14.0))
+    W[2, 5] = W[5, 2] = 0.25
+    d, f = _weights(W, 13, "Q")
+    np.testing.assert_array_equal(f, W)
+    W[2, 5] = 0.3
+    with pytest.raises(ValueError, match="not symmetric"):
+        _weights(W, 13, "Q")
 
 
 class LinearMpcConfig16(LinearMpcConfig):   # the reference default: horizon = 16 (linear_mpc_configs.py:11)
