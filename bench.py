@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--config", default="config2", choices=sorted(CONFIGS) + ["config1"])
     ap.add_argument("--standing-every", type=int, default=0,
                     help="diagnostics: make every k-th robot stand (the interior-point class)")
+    ap.add_argument("--gait", default="trot10",
+                    help="config1: the drop-in's gait (trot10 = Gait.TROTTING10; standing = Gait.STANDING, "
+                         "the interior-point class at horizon 16)")
     ap.add_argument("--total", type=int, default=0, help="--rehearse-cpu: global robots (uneven shards)")
     ap.add_argument("--rehearse-cpu", action="store_true",
                     help="no GPU: rehearse the rank / shard / gather logic over gloo with a stand-in "
@@ -293,7 +296,7 @@ def bench_config1(args):
     v_des = np.array([1.2, 0.0, 0.0])
     for it in range(n_iter):
         rd = _SyntheticRobotData(it * 1e-3)
-        table = gait_table("trot10", (it // 20) % 10, N).reshape(-1)
+        table = gait_table(args.gait, (it // 20) % 10, N).reshape(-1)
         t0 = time.perf_counter()
         ctl.update_robot_state(rd)
         u = ctl.update_mpc_if_needed(it, v_des, 0.0, table, solver="drake")
@@ -323,11 +326,12 @@ def bench_config1(args):
                          "(oracle/cpu_mpc.cpp)"}
     med = float(np.median(mpc_ms))
     print(json.dumps({
-        "metric": "drop-in MPC tick latency (B=1, Aliengo, horizon 16, trot10)",
+        "metric": f"drop-in MPC tick latency (B=1, Aliengo, horizon 16, {args.gait})",
         "value": med, "unit": "ms", "n_gpus": 1, "steps": len(mpc_ms), "warmup": args.warmup,
         "higher_is_better": False, "dtype": "f64", "data": "synthetic Aliengo trot states (no simulator)",
         "config": {"workload": "config1: ModelPredictiveController drop-in, scripts/mujoco_aliengo.py loop, "
-                               "LinearMpcConfig.horizon = 16, Gait.TROTTING10", "batch": 1, "horizon": N},
+                               f"LinearMpcConfig.horizon = 16, gait {args.gait}", "batch": 1, "horizon": N,
+                   "gait": args.gait},
         "mpc_tick_ms": {"median": med, "p90": float(np.percentile(mpc_ms, 90)), "mean": float(np.mean(mpc_ms))},
         "other_tick_ms": {"median": float(np.median(other_ms)), "p90": float(np.percentile(other_ms, 90))},
         "cpu_baseline": cpu,

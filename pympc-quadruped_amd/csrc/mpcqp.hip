@@ -397,7 +397,8 @@ __global__ __launch_bounds__(Cfg<128>::NT) void mpcqp_kernel_128(
 
 // Large class (n > 128: standing schedules at N >= 11): one wave per queued robot,
 // Riccati-factored interior point + active-set polish (mpcqp_ipm.h).  Same launch /
-// reset protocol as class 128.
+// reset protocol as class 128.  FULL: non-diagonal weights (mpcqp_set_weights).
+template <bool FULL>
 __global__ __launch_bounds__(LANES) void mpcqp_kernel_ipm(
     KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
@@ -407,13 +408,13 @@ __global__ __launch_bounds__(LANES) void mpcqp_kernel_ipm(
   const int tid = threadIdx.x;
   const int k = blockIdx.x;
   if (direct_B > 0) {
-    if (k < direct_B) solve_robot_ipm(P, k, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg);
+    if (k < direct_B) solve_robot_ipm<FULL>(P, k, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg);
     return;
   }
   const int cnt = uni(__hip_atomic_load(&queue[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (k < cnt) {
     const int b = uni(queue[4 + k]);
-    solve_robot_ipm(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg);
+    solve_robot_ipm<FULL>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg);
     if (tid == 0 && atomicAdd(&queue[2], 1) == cnt - 1) {
       atomicExch(&queue[0], 0);
       atomicExch(&queue[2], 0);
@@ -661,7 +662,7 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   const bool fork = giant && first < 3 && side_stream(qs);
   bool ipm_done = false;
   auto launch_ipm = [&](hipStream_t s) -> hipError_t {
-    hipLaunchKernelGGL(mpcqp_kernel_ipm, dim3(batch), dim3(LANES), 0, s, kp, x0, xref, contact, feet, robot, u0, U,
+    hipLaunchKernelGGL(full ? mpcqp_kernel_ipm<true> : mpcqp_kernel_ipm<false>, dim3(batch), dim3(LANES), 0, s, kp, x0, xref, contact, feet, robot, u0, U,
                        (int*)status, (int*)iters, q + 2 * (4 + (size_t)cap), first == 3 ? (int)batch : 0);
     ipm_done = true;
     return hipGetLastError();

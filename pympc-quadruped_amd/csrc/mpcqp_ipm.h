@@ -136,6 +136,7 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 }
 
 // One robot with more than 128 stance variables.  Called by a 64-thread workgroup.
+template <bool FULL>
 __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmShared& sm,
                                                 const float* __restrict__ x0g, const float* __restrict__ xrefg,
                                                 const float* __restrict__ contactg, const float* __restrict__ feetg,
@@ -160,7 +161,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     write_empty_t<NT>(b, lane, N, MPCQP_STATUS_OK, u0g, Ug, statusg, itersg);
     return;
   }
-  if (KP.wfull) {   // full weights: cross-leg R couplings break the per-foot-step weights
+  if constexpr (FULL) {   // full weights: cross-leg R couplings break the per-foot-step weights
     bool cross = false;
     for (int e = lane; e < NU * NU; e += NT)
       cross |= (e / NU) / 3 != (e % NU) / 3 && KP.wfull[NX * NX + e] != 0.0;
@@ -194,13 +195,9 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       sm.qh[lane] = 2.0 * KP.q[lane];
     }
     if (lane < NU) sm.rh[lane] = 2.0 * KP.r[lane];
-    for (int e = lane; e < NX * NX; e += NT) {
-      const int i = e / NX, j = e % NX;
-      sm.qf[i][j] = KP.wfull ? 2.0 * KP.wfull[e] : (i == j ? 2.0 * KP.q[i] : 0.0);
-    }
-    for (int e = lane; e < NU * NU; e += NT) {
-      const int i = e / NU, j = e % NU;
-      sm.rf[i][j] = KP.wfull ? 2.0 * KP.wfull[NX * NX + e] : (i == j ? 2.0 * KP.r[i] : 0.0);
+    if constexpr (FULL) {
+      for (int e = lane; e < NX * NX; e += NT) sm.qf[e / NX][e % NX] = 2.0 * KP.wfull[e];
+      for (int e = lane; e < NU * NU; e += NT) sm.rf[e / NU][e % NU] = 2.0 * KP.wfull[NX * NX + e];
     }
     for (int e = lane; e < N * NX; e += NT) sm.xr[e / NX][e % NX] = (double)smf.in[IN_XREF + e];
     for (int e = lane; e < N * NU; e += NT) sm.U[e / NU][e % NU] = 0.0;
@@ -226,12 +223,19 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     o[2] = p[2];
   };
   auto foot_ptr = [&](int j, double (*A)[NU]) -> double* { return &A[sm.mt.foot_t[j]][3 * sm.mt.foot_leg[j]]; };
-  auto legrh = [&](int j, double (&o)[9]) {   // the leg's 3 x 3 block of Rh
+  constexpr int kRh = FULL ? 9 : 3;   // the leg's 3 x 3 block of Rh, or its diagonal
+  auto legrh = [&](int j, double (&o)[kRh]) {
     const int l = sm.mt.foot_leg[j];
+    if constexpr (FULL) {
 #pragma unroll
-    for (int x = 0; x < 3; ++x)
+      for (int x = 0; x < 3; ++x)
 #pragma unroll
-      for (int y = 0; y < 3; ++y) o[3 * x + y] = sm.rf[3 * l + x][3 * l + y];
+        for (int y = 0; y < 3; ++y) o[3 * x + y] = sm.rf[3 * l + x][3 * l + y];
+    } else {
+      o[0] = sm.rh[3 * l];
+      o[1] = sm.rh[3 * l + 1];
+      o[2] = sm.rh[3 * l + 2];
+    }
   };
 
 #ifdef MPCQP_IPM_DEBUG
@@ -313,9 +317,13 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     const int li = lane < NX ? lane : 0;
     for (int k = N - 1; k >= 0; --k) {
       double v = 0.0;
-      if (lane < NX) {
+      if constexpr (FULL) {
+        if (lane < NX) {
 #pragma unroll
-        for (int j = 0; j < NX; ++j) v = fma(sm.qf[li][j], sm.X[k + 1][j] - sm.xr[k][j], v);
+          for (int j = 0; j < NX; ++j) v = fma(sm.qf[li][j], sm.X[k + 1][j] - sm.xr[k][j], v);
+        }
+      } else {
+        v = lane < NX ? sm.qh[li] * (sm.X[k + 1][li] - sm.xr[k][li]) : 0.0;
       }
       if (k < N - 1) {
         double s[7];
@@ -333,9 +341,13 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       double bcl[12], nv[12];
       ld12(bcl, sm.BmT[c]);
       ld12(nv, sm.nuh[k]);
-      const int c3 = 3 * (c / 3);   // Rh's leg block (no cross-leg couplings in this class)
-      const double ru = fma(sm.rf[c][c3 + 2], sm.U[k][c3 + 2],
-                            fma(sm.rf[c][c3 + 1], sm.U[k][c3 + 1], sm.rf[c][c3] * sm.U[k][c3]));
+      double ru;
+      if constexpr (FULL) {
+        const int c3 = 3 * (c / 3);   // Rh's leg block (no cross-leg couplings in this class)
+        ru = fma(sm.rf[c][c3 + 2], sm.U[k][c3 + 2], fma(sm.rf[c][c3 + 1], sm.U[k][c3 + 1], sm.rf[c][c3] * sm.U[k][c3]));
+      } else {
+        ru = sm.rh[c] * sm.U[k][c];
+      }
       const double g = ru + dot12(bcl, nv);
       sm.gr[k][c] = sm.mt.stance_of[4 * k + c / 3] >= 0 ? g : 0.0;
     }
@@ -376,16 +388,20 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
 #pragma unroll
     for (int a2 = 0; a2 < 3; ++a2) bx[q][a2] = ok ? sm.Bm[lcc][3 * (cc / 3) + a2] : 0.0;
   }
-  auto qhat4 = [&]() -> d4 {   // Qh's 12 x 12 moving-state block in result layout
-    d4 v;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = (lr + 4 * i < 12 && lc < 12) ? sm.qf[lr + 4 * i][lc] : 0.0;
-    return v;
-  };
   auto diag4 = [&](double d) -> d4 {   // d I (12 x 12) in result layout
     d4 v;
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = (lr + 4 * i == lc && lc < 12) ? d : 0.0;
+    return v;
+  };
+  auto qhat4 = [&]() -> d4 {   // Qh's 12 x 12 moving-state block in result layout
+    d4 v;
+    if constexpr (FULL) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = (lr + 4 * i < 12 && lc < 12) ? sm.qf[lr + 4 * i][lc] : 0.0;
+    } else {
+      v = diag4(sm.qh[lcc]);
+    }
     return v;
   };
   auto mfma = [](double a, double b, d4 c) -> d4 { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); };
@@ -663,7 +679,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
 
   // ---- start: minimiser under a mild barrier weight, slacks shifted into the interior
   for (int j = lane; j < S; j += NT) {
-    double d[6], rh[9], wv[9];
+    double d[6], rh[kRh], wv[9];
 #pragma unroll
     for (int r = 0; r < 6; ++r) d[r] = 1e-2;
     legrh(j, rh);
@@ -694,7 +710,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
   // ---- active-set polish on the rows sm.fact; true when verified (sm.U = the optimum)
   auto polish = [&]() -> bool {
     for (int j = lane; j < S; j += NT) {
-      double rh[9], pj[9], fp[3], wv[9];
+      double rh[kRh], pj[9], fp[3], wv[9];
       legrh(j, rh);
       ipm_foot_nullspace(rw, sm.fact[j] & liv, -sm.mt.ub[j], rh, pj, fp, wv);
 #pragma unroll
@@ -756,7 +772,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       double best = INFINITY;
       int drop = -1;
       if (am) {
-        double pjl[9], fpd[3], wd[9], rh[9];
+        double pjl[9], fpd[3], wd[9], rh[kRh];
         legrh(j, rh);
         const int nq = ipm_foot_nullspace(rw, am, h5, rh, pjl, fpd, wd);
         ipm_cone_multipliers(rw, am, nq, g, tol_g, best, drop);
@@ -842,7 +858,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       fsync<NT>();
     }
     for (int j = lane; j < S; j += NT) {
-      double d[6], rh[9], wv[9];
+      double d[6], rh[kRh], wv[9];
 #pragma unroll
       for (int r = 0; r < 6; ++r) d[r] = ((liv >> r) & 1) ? sm.fl[j][r] / sm.fs[j][r] : 0.0;
       legrh(j, rh);

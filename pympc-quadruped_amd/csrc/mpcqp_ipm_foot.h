@@ -9,7 +9,7 @@
 #endif
 
 // 3x3 inverse by the adjugate (symmetric positive definite arguments)
-__host__ __device__ inline __attribute__((always_inline)) void inv3(const double (&a)[9], double (&o)[9]) {
+__host__ __device__ inline void inv3(const double (&a)[9], double (&o)[9]) {
   const double c00 = a[4] * a[8] - a[5] * a[7], c01 = a[5] * a[6] - a[3] * a[8], c02 = a[3] * a[7] - a[4] * a[6];
   const double det = a[0] * c00 + a[1] * c01 + a[2] * c02;
   const double id = 1.0 / det;
@@ -29,7 +29,7 @@ __host__ __device__ inline __attribute__((always_inline)) void inv3(const double
 // g = sum lambda_r a_r (Caratheodory: g is in the cone of the active rows iff some such
 // subset has lambda >= 0).  best = -inf when no subset reproduces g; drop = the row of
 // the best subset's most negative multiplier when best < -tol.
-__host__ __device__ inline __attribute__((always_inline)) void ipm_cone_multipliers(const double (&rw)[6][3], int am, int nq, const double (&g)[3],
+__host__ __device__ inline void ipm_cone_multipliers(const double (&rw)[6][3], int am, int nq, const double (&g)[3],
                                                      double tol, double& best, int& drop) {
   best = -INFINITY;
   drop = -1;
@@ -95,9 +95,81 @@ __host__ __device__ inline __attribute__((always_inline)) void ipm_cone_multipli
 // only one with a non-zero right-hand side h5), dependent rows skipped.  Outputs the
 // projector pj = I - sum q q^T onto the null space, the minimum-norm particular
 // solution fp of the independent active rows (a_r . fp = h_r), and the weight
-// W = pj (pj Rh pj + I - pj)^-1 pj of the reduced stage problem (rh: the leg's 3 x 3
-// block of the input weights, row-major).  Returns the rank (0..3).
-__host__ __device__ inline __attribute__((always_inline)) int ipm_foot_nullspace(const double (&rw)[6][3], int am, double h5, const double (&rh)[9],
+// W = pj (pj Rh pj + I - pj)^-1 pj of the reduced stage problem (rh: the leg's 3
+// diagonal input weights).  Returns the rank (0..3).
+__host__ __device__ inline int ipm_foot_nullspace(const double (&rw)[6][3], int am, double h5, const double (&rh)[3],
+                                                  double (&pj)[9], double (&fp)[3], double (&W)[9]) {
+  double q0[3] = {0.0, 0.0, 0.0}, q1[3] = {0.0, 0.0, 0.0}, q2[3] = {0.0, 0.0, 0.0};
+  double c0 = 0.0, c1 = 0.0, c2 = 0.0;   // L c = h over the independent rows (forward substitution)
+  int nq = 0;
+  for (int o = 0; o < 6; ++o) {
+    const int r = o == 0 ? 5 : o - 1;
+    if (!((am >> r) & 1) || nq == 3) continue;
+    double v[3] = {rw[r][0], rw[r][1], rw[r][2]};
+    const double n0 = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    const double hr = r == 5 ? h5 : 0.0;
+    double l0 = 0.0, l1 = 0.0;
+    if (nq >= 1) {
+      l0 = q0[0] * v[0] + q0[1] * v[1] + q0[2] * v[2];
+      for (int x = 0; x < 3; ++x) v[x] -= l0 * q0[x];
+    }
+    if (nq >= 2) {
+      l1 = q1[0] * v[0] + q1[1] * v[1] + q1[2] * v[2];
+      for (int x = 0; x < 3; ++x) v[x] -= l1 * q1[x];
+    }
+    const double nv = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    if (!(nv > 1e-9 * n0)) continue;   // dependent on the rows already taken
+    if (nq == 0) {
+      for (int x = 0; x < 3; ++x) q0[x] = v[x] / nv;
+      c0 = hr / nv;
+    } else if (nq == 1) {
+      for (int x = 0; x < 3; ++x) q1[x] = v[x] / nv;
+      c1 = (hr - l0 * c0) / nv;
+    } else {
+      for (int x = 0; x < 3; ++x) q2[x] = v[x] / nv;
+      c2 = (hr - l0 * c0 - l1 * c1) / nv;
+    }
+    ++nq;
+  }
+  for (int x = 0; x < 3; ++x) {
+    fp[x] = c0 * q0[x] + c1 * q1[x] + c2 * q2[x];
+    for (int y = 0; y < 3; ++y)
+      pj[3 * x + y] = ((x == y) ? 1.0 : 0.0) - q0[x] * q0[y] - q1[x] * q1[y] - q2[x] * q2[y];
+  }
+  double a[9], o[9], t[9];
+  for (int x = 0; x < 3; ++x)
+    for (int y = 0; y < 3; ++y) {
+      double v = ((x == y) ? 1.0 : 0.0) - pj[3 * x + y];
+      for (int z = 0; z < 3; ++z) v += pj[3 * x + z] * rh[z] * pj[3 * z + y];
+      a[3 * x + y] = v;
+    }
+  inv3(a, o);
+  for (int x = 0; x < 3; ++x)
+    for (int y = 0; y < 3; ++y) t[3 * x + y] = o[3 * x] * pj[y] + o[3 * x + 1] * pj[3 + y] + o[3 * x + 2] * pj[6 + y];
+  for (int x = 0; x < 3; ++x)
+    for (int y = 0; y < 3; ++y)
+      W[3 * x + y] = pj[3 * x] * t[y] + pj[3 * x + 1] * t[3 + y] + pj[3 * x + 2] * t[6 + y];
+  return nq;
+}
+
+// Interior-point weight of a foot-step: W = (diag(rh) + sum_r d_r a_r a_r^T)^-1 over the
+// rows in `live` (bit r).
+__host__ __device__ inline void ipm_foot_weight(const double (&rw)[6][3], int live, const double (&d)[6],
+                                                const double (&rh)[3], double (&W)[9]) {
+  double a[9];
+  for (int x = 0; x < 3; ++x)
+    for (int y = 0; y < 3; ++y) {
+      double v = (x == y) ? rh[x] : 0.0;
+      for (int r = 0; r < 6; ++r)
+        if ((live >> r) & 1) v += d[r] * rw[r][x] * rw[r][y];
+      a[3 * x + y] = v;
+    }
+  inv3(a, W);
+}
+
+// ipm_foot_nullspace with the leg's full 3 x 3 block of the input weights (row-major;
+// mpcqp_set_weights): W = pj (pj Rh pj + I - pj)^-1 pj.
+__host__ __device__ inline int ipm_foot_nullspace(const double (&rw)[6][3], int am, double h5, const double (&rh)[9],
                                                   double (&pj)[9], double (&fp)[3], double (&W)[9]) {
   double q0[3] = {0.0, 0.0, 0.0}, q1[3] = {0.0, 0.0, 0.0}, q2[3] = {0.0, 0.0, 0.0};
   double c0 = 0.0, c1 = 0.0, c2 = 0.0;   // L c = h over the independent rows (forward substitution)
@@ -153,9 +225,8 @@ __host__ __device__ inline __attribute__((always_inline)) int ipm_foot_nullspace
   return nq;
 }
 
-// Interior-point weight of a foot-step: W = (Rh_leg + sum_r d_r a_r a_r^T)^-1 over the
-// rows in `live` (bit r); rh: the leg's 3 x 3 block of the input weights, row-major.
-__host__ __device__ inline __attribute__((always_inline)) void ipm_foot_weight(const double (&rw)[6][3], int live, const double (&d)[6],
+// The same with the leg's full 3 x 3 block of the input weights (row-major; mpcqp_set_weights).
+__host__ __device__ inline void ipm_foot_weight(const double (&rw)[6][3], int live, const double (&d)[6],
                                                 const double (&rh)[9], double (&W)[9]) {
   double a[9];
   for (int x = 0; x < 3; ++x)
