@@ -20,6 +20,8 @@ SURVEY.md Appendix A), then:
                         (kinematics.py:40-71) on float32 quaternions, and
                         LegController.update's stance branch (leg_controller.py:86-89)
 
+  formulation_full_N{N}.npz  the same for full (non-diagonal) Q and R (--full N)
+
 Usage:  python tests/golden/make_golden.py            (all horizons, subprocesses)
         python tests/golden/make_golden.py --horizon 10
         python tests/golden/make_golden.py --planner       (planner.npz only)
@@ -129,6 +131,73 @@ def gen(horizon):
     if N == 16:
         gen_reftraj(LinearMpcConfig, robot_configs, mpc)
     print(f"N={N}: max KKT {np.array(kkts).max():.2e}, iterations {iters}")
+
+
+def full_weights(seed):
+    """A symmetric positive-semidefinite Q coupling the moving state components (the
+    reference's diagonal scaled by a correlation matrix, |rho| <= 0.4; state 12 keeps
+    weight 0) and an R with full 3 x 3 leg blocks (mpc.py:49-52 take whole matrices)."""
+    rng = np.random.default_rng(seed)
+    C = np.eye(13)
+    for _ in range(12):
+        i, j = rng.choice(12, size=2, replace=False)
+        C[i, j] = C[j, i] = rng.uniform(-0.4, 0.4)
+    w, V = np.linalg.eigh(C)
+    C = V @ np.diag(np.maximum(w, 0.05)) @ V.T
+    d = np.sqrt(np.diag(C))
+    C = C / np.outer(d, d)
+    sq = np.sqrt(np.array([5., 5., 10., 10., 10., 50., 0.01, 0.01, 0.2, 0.2, 0.2, 0.2, 0.]))
+    Q = np.outer(sq, sq) * C
+    R = np.diag([1e-5] * 12)
+    for leg in range(4):
+        S = rng.uniform(-0.3, 0.3, size=(3, 3))
+        R[3 * leg:3 * leg + 3, 3 * leg:3 * leg + 3] += 1e-5 * (S @ S.T)
+    return 0.5 * (Q + Q.T), 0.5 * (R + R.T)
+
+
+def gen_full(horizon):
+    """formulation_full_N{N}.npz: the reference's own H, g for full (non-diagonal) Q and R
+    (a LinearMpcConfig subclass carrying them, mpc.py:49-52), and the exact optimum u* of
+    that QP -- pins the oracle's and the engine's general-weight path."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "pympc-quadruped_amd")]
+    LinearMpcConfig, robot_configs, mpc, gait = stub_reference(horizon)
+    from oracle import qp as Q
+    from mpcqp.synthetic import make_batch
+    from mpcqp.params import robot_from_config
+    N = horizon
+    Qf, Rf = full_weights(500 + N)
+
+    class FullWeights(LinearMpcConfig):
+        Q = Qf
+        R = Rf
+
+    cfgs = {"a1": robot_configs.A1Config, "aliengo": robot_configs.AliengoConfig}
+    B = 8
+    bt = make_batch(B, N, seed=5151 + N, gaits=("trot10", "pace10", "bound8", "standing"), robots=("a1", "aliengo"))
+    names, Hp, gs, us = [], [], [], []
+    probe = np.random.default_rng(98).standard_normal((2, 12 * N))
+    for b in range(B):
+        nm = "a1" if abs(bt["robot"][b][0] - 4.713) < 1e-3 else "aliengo"
+        names.append(nm)
+        bt["robot"][b] = robot_from_config(cfgs[nm])
+        c = mpc.ModelPredictiveController(FullWeights, cfgs[nm])
+        x0 = bt["x0"][b].copy()
+        c.current_state = x0
+        c.yaw = float(x0[2])
+        c.pos_base_feet = [bt["feet"][b][i].astype(np.float64) for i in range(4)]
+        Ac, Bc = c._generate_state_space_model()
+        Ad, Bd = c._discretize_continuous_model(Ac, Bc)
+        H, g = c._generate_QP_cost(Ad, Bd, c.current_state, bt["xref"][b].reshape(-1))
+        C, lb, ub = c._generate_QP_constraints(bt["contact"][b].reshape(-1))
+        x, _, _ = Q.solve_qp_dual_active_set(H, g, C, lb, ub)
+        Hp.append([H @ v for v in probe])
+        gs.append(g)
+        us.append(x)
+    np.savez_compressed(os.path.join(HERE, f"formulation_full_N{N}.npz"), x0=bt["x0"], xref=bt["xref"],
+                        contact=bt["contact"], feet=bt["feet"], robot=bt["robot"], robot_name=np.array(names),
+                        Q=Qf, R=Rf, H_probe=np.array(Hp), probe=probe, g=np.array(gs), u_star=np.array(us),
+                        horizon=N, dt=0.05)
+    print(f"full weights N={N}: {B} cases")
 
 
 class _FakeRobotData:
@@ -278,8 +347,11 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--horizon", type=int, default=0)
     ap.add_argument("--planner", action="store_true")
+    ap.add_argument("--full", type=int, default=0, help="formulation_full_N{N}.npz only")
     a = ap.parse_args()
-    if a.planner:
+    if a.full:
+        gen_full(a.full)
+    elif a.planner:
         gen_planner()
     elif a.horizon:
         gen(a.horizon)

@@ -73,6 +73,23 @@ def test_reference_golden_fixtures(N):
     assert worst < TOL_ACHIEVED, worst
 
 
+@pytest.mark.parametrize("N", [10, 16])
+def test_reference_golden_full_weights(N):
+    """u* of QPs the reference builds with full (non-diagonal) Q and leg-block R
+    (formulation_full_N{N}.npz, mpc.py:49-52): the engine takes the same matrices
+    (mpcqp_set_weights); N = 16 includes standing robots (the interior-point class)."""
+    z = np.load(os.path.join(GOLDEN, f"formulation_full_N{N}.npz"), allow_pickle=False)
+    bt = {k: z[k] for k in ("x0", "xref", "contact", "feet", "robot")}
+    u0, U, status, _ = _solve(_engine(N, Q=z["Q"], R=z["R"]), bt)
+    worst = 0.0
+    for b in range(len(bt["x0"])):
+        assert status[b] == 0, (b, status)
+        e = max(rel_err_u0(u0[b], z["u_star"][b][:12]), rel_err_u0(U[b], z["u_star"][b]))
+        assert e < TOL_U0, (b, e)
+        worst = max(worst, e)
+    assert worst < TOL_ACHIEVED, worst
+
+
 def test_edge_cases():
     from mpcqp.synthetic import make_batch
     N = 10
