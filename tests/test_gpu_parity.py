@@ -233,6 +233,35 @@ def test_capacity_class_routing():
     assert all(st[b] == 0 for b in (0, 3, 5, 6, 7))
 
 
+def test_class64_capacity_boundary():
+    """Both sides of class 64's capacity (n = 60 / 63 / 66 at N = 10: 20 / 21 / 22 stance
+    foot-steps), with and without a stance range that launches the first possible class
+    directly, match the oracle."""
+    from mpcqp.synthetic import make_batch
+    N = 10
+    bt = make_batch(6, N, seed=63, gaits=("trot10",), robots=("a1",))
+    bt["contact"][0] = 0.0
+    bt["contact"][0].reshape(-1)[:21] = 1.0        # n = 63
+    bt["contact"][1] = 0.0
+    bt["contact"][1].reshape(-1)[:20] = 1.0        # n = 60
+    bt["contact"][2] = 0.0
+    bt["contact"][2].reshape(-1)[::2] = 1.0        # n = 60, alternating feet
+    bt["contact"][3] = 0.0
+    bt["contact"][3].reshape(-1)[:22] = 1.0        # n = 66: class 96
+    ns = 3 * (bt["contact"] > 0).reshape(6, -1).sum(1)
+    assert ns[0] == 63 and ns[1] == 60 and ns[2] == 60 and ns[3] == 66
+    for rng in ((0, 0), (20, 21), (21, 21), (22, 22)):
+        eng = _engine(N)
+        eng.set_stance_range(*rng)
+        sel = [b for b in range(6) if rng == (0, 0) or rng[0] <= ns[b] // 3 <= rng[1]]
+        sub = {k: v[sel] for k, v in bt.items()}
+        u0, U, status, _ = _solve(eng, sub)
+        assert (status == 0).all(), (rng, status)
+        for i, b in enumerate(sel):
+            x, _, _ = oracle_solution(bt, b, N)
+            assert rel_err_u0(U[i], x) < TOL_ACHIEVED, (rng, b, rel_err_u0(U[i], x))
+
+
 def test_two_streams_no_host_sync():
     """One context, two streams, no host synchronisation between the calls: each
     stream has its own device queues, so robots of the queued classes (N = 16 trot /
