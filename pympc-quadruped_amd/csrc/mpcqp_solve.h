@@ -596,13 +596,16 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         }
         if constexpr (kSplit) {
           if (lane == 0)
-            *(volatile int*)&sm.choice = (((it + 1) & 0xffff) << 16) | ((pc2 + 1) << 8) | (pc + 1);
+            // relaxed workgroup-scope atomics, not volatile: a volatile access keeps the
+            // generic address space (a FLAT load / store with a vmcnt wait); these stay DS ops
+            __hip_atomic_store(&sm.choice, (((it + 1) & 0xffff) << 16) | ((pc2 + 1) << 8) | (pc + 1),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       } else {
         const int tag = (it + 1) & 0xffff;
         int w;
         do {
-          w = uni(*(volatile int*)&sm.choice);
+          w = uni(__hip_atomic_load(&sm.choice, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
         } while ((w >> 16) != tag);
         pc = (w & 0xff) - 1;
         pc2 = ((w >> 8) & 0xff) - 1;
