@@ -49,6 +49,12 @@ static_assert(kMaxN == 20, "the dense classes' and the interior-point class's LD
 #ifndef MPCQP_SPLIT_CHOICE
 #define MPCQP_SPLIT_CHOICE 1   // class 64: wave 1 chooses the next rows, wave 0 reads them; 0: both choose
 #endif
+#ifndef MPCQP_PAIR_MAX_NV
+#define MPCQP_PAIR_MAX_NV 96   // pair steps in classes 64 and 96 (class 128: no VGPRs to spare)
+#endif
+#ifndef MPCQP_CURKEY_MAX_NV
+#define MPCQP_CURKEY_MAX_NV 64   // row choice in the current projected metric up to this class
+#endif
 #ifndef MPCQP_SWEEP_MFMA
 #define MPCQP_SWEEP_MFMA 0   // 1: class-64 H^-1 sweep blocked by 4 pivots on the f64 MFMA (parity-exact, slower: DESIGN 4.5)
 #endif

@@ -54,7 +54,7 @@ struct alignas(16) SharedT {
 #ifdef MPCQP_NO_PAIR
   static constexpr bool kPair = false;
 #else
-  static constexpr bool kPair = NV == 64;   // class 128 has no VGPRs to spare for pair steps
+  static constexpr bool kPair = NV <= MPCQP_PAIR_MAX_NV;   // class 128 has no VGPRs to spare for pair steps
 #endif
   union {
     FormArea<NV> fa;
@@ -490,7 +490,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   double s[CPL];
   // classes 96 / 128 keep the initial metric: their launches are throughput-bound and
   // the per-pass updates cost more than the passes they save (configs 4 / 5: -3 / -1 %)
-  constexpr bool kCurKey = NV == 64;
+  constexpr bool kCurKey = NV <= MPCQP_CURKEY_MAX_NV;
   float qm[CPL];   // a_c^T P a_c (f32; classes 96 / 128: 1 / sqrt(a_c^T W a_c)): scales the f32 row key
   auto cdot = [&](const double* v, int k) -> double {
     const double* a = sm.mt.rows[crt[k]];

@@ -6,7 +6,8 @@ rows from distinct foot-steps added at once when the equality-constrained step
 keeps every multiplier positive (nested fallback to fewer rows, then a single
 GI step).  Decisions follow the engine: the most violated row in the dual metric
 (scaled by the initial W), partner rows the best of other foot-steps.
-Usage: python tools/gi_sim.py [B] [k ...]   (GI_METRIC=W: rows keyed in the initial metric)
+Usage: python tools/gi_sim.py [B] [k ...]   (GI_METRIC=W: rows keyed in the initial metric;
+GI_N / GI_GAITS: horizon and gait mix, default 10 / trot10)
 """
 import os
 import sys
@@ -201,8 +202,8 @@ def simulate(H, g, A, b, foot, kmax, tol=1e-9, max_pass=2000, ratio=0.0, stop_af
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
     ks = [a for a in sys.argv[2:]] or ["1", "2", "3", "4"]
-    N = 10
-    bt = make_batch(B, N, seed=1000, gaits=("trot10",), robots=("a1",))
+    N = int(os.environ.get("GI_N", "10"))   # GI_N=16 GI_GAITS=trot10,pace10,bound8: the config-4 mix
+    bt = make_batch(B, N, seed=1000, gaits=tuple(os.environ.get("GI_GAITS", "trot10").split(",")), robots=("a1",))
     qps = [robot_qp(bt, b, N) for b in range(B)]
     ref = None
     for ka in ks:
