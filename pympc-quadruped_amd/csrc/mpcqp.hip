@@ -58,6 +58,19 @@ static_assert(kMaxN == 20, "the dense classes' and the interior-point class's LD
 #ifndef MPCQP_SWEEP_MFMA
 #define MPCQP_SWEEP_MFMA 0   // 1: class-64 H^-1 sweep blocked by 4 pivots on the f64 MFMA (parity-exact, slower: DESIGN 4.5)
 #endif
+#ifndef MPCQP_C64_SYMSWEEP
+// 1: class 64 takes n <= 60 and inverts H on ONE wave holding its 64 lower 4 x 8 tiles
+// (no barrier per pivot, half the VALU of the two-wave sweep); n = 61..64 go to class 96
+#define MPCQP_C64_SYMSWEEP 0   // measured slower: off
+#endif
+#ifndef MPCQP_EARLY_CHOICE
+// class 64 split choice: wave 1 chooses the next rows as soon as the pass has updated the
+// row values, before its rank-1 / rank-2 FMAs, so wave 0 finds the choice published
+#define MPCQP_EARLY_CHOICE 1
+#endif
+#ifndef MPCQP_C64_SYMPAIR
+#define MPCQP_C64_SYMPAIR 1   // the one-wave sweep takes pivot pairs (one rank-2 pass each)
+#endif
 #ifndef MPCQP_C64_WPE
 #define MPCQP_C64_WPE (MPCQP_C64_TW == 4 ? 4 : 2)   // class-64 waves per SIMD (VGPR budget)
 #endif
@@ -322,6 +335,9 @@ __device__ __forceinline__ int xcd_robot(int bid, int B) {
   const int x = bid & 7, i = bid >> 3, q = B >> 3, r = B & 7;
   return x * q + (x < r ? x : r) + i;
 }
+
+// class 64's capacity (stance variables): 60 with the one-wave symmetric sweep
+constexpr int kCap64 = MPCQP_C64_SYMSWEEP ? 60 : 64;
 
 // Class NV = 64: one 2-wave workgroup per robot of the batch.  Robots with more
 // than 64 stance variables are appended to `queue` (when given) for class 96, those
@@ -650,9 +666,9 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   const int nmax_h = 12 * kp.N;
   const int nmax = ctx->stance_hint > 0 && 3 * ctx->stance_hint < nmax_h ? 3 * ctx->stance_hint : nmax_h;
   const int nmin = 3 * ctx->stance_min;
-  const bool large = nmax > 64, huge = nmax > 96, giant = nmax > 128;
+  const bool large = nmax > kCap64, huge = nmax > 96, giant = nmax > 128;
   // the first class launched: 0 = class 64, 1 = 96, 2 = 128, 3 = interior point
-  const int first = nmin > 128 ? 3 : nmin > 96 ? 2 : nmin > 64 ? 1 : 0;
+  const int first = nmin > 128 ? 3 : nmin > 96 ? 2 : nmin > kCap64 ? 1 : 0;
   int* q = nullptr;
   QueueSet* qs = nullptr;
   int cap = 0;

@@ -94,6 +94,14 @@ __device__ __forceinline__ double dpp_shl1(double v) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// Class 64 with the one-wave sweep: a symmetric 60 x 60 matrix (64 x 64 with padding)
+// held as its 64 lower 4 x 8 tiles (tile rows br < 15, tile columns bc <= br / 2, in
+// row-major order): tile L = lt_idx(br, bc), element 8 r + c at base[(8 r + c) * 64 + L]
+__device__ __forceinline__ int lt_idx(int br, int bc) {
+  const int m = br >> 1;
+  return ((br & 1) ? (m + 1) * (m + 1) : m * (m + 1)) + bc;
+}
+
 // Sum 4 row partials over the TCN lanes of a tile row.  Lane keeps row
 // 4tr + 2 bit2(lane) + bit1(lane) (see trow / twriter).
 template <int TCN>
@@ -193,6 +201,9 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   int seccur_ = 7;
 #endif
   STAMP(0);
+#ifdef MPCQP_STAMPS
+  const unsigned long long rt0_ = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide
+#endif
 
   // ------------------------------------------------ inputs, stance list
   Form& smf = sm.fa.f;
@@ -205,7 +216,10 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   fsync<NT>();
   const int S = uni(sm.mt.S);
   const int n = 3 * S, m = 6 * S;
-  if (n > NV) {
+  // class 64 with the one-wave symmetric sweep holds n <= 60 (15 tile rows: 64 lower tiles)
+  constexpr bool kSym = NV == 64 && MPCQP_C64_SYMSWEEP && TW == 8 && C::NW == 2;
+  constexpr int kCap = kSym ? 60 : NV;
+  if (n > kCap) {
     // the next capacity class takes it: `queue`, `queue_big` (when given) for a robot
     // beyond class 96 as well, `queue_ipm` (when given) for one beyond class 128
     int* qn = queue;
@@ -262,7 +276,17 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   }
   constexpr bool kMfmaSweep = NV == 64 && MPCQP_SWEEP_MFMA;
   fsync<NT>();   // every lane is done reading the formulation scratch H overwrites
-  if constexpr (!kMfmaSweep) {
+  if constexpr (kSym) {
+    // H's 64 lower tiles (tile rows < 15, tc <= tr / 2) into the first half of ht; the
+    // second half stages the sweep's result
+    // (unconditional stores: the other lanes write into the still-dead staging half, so the
+    // H build is not sunk into a branch -- in the full-weight kernel that spilled)
+    const int L = (tr < 15 && tc <= (tr >> 1)) ? lt_idx(tr, tc) : 2048 + lane;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < TW; ++c) sm.ht[(TW * r + c) * LANES + L] = W[r][c];
+  } else if constexpr (!kMfmaSweep) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -271,7 +295,193 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   STAMP(2);
 
   // ------------------------------------------------ W = H^-1 (symmetric sweep)
-  if constexpr (kMfmaSweep) {
+  if constexpr (kSym) {
+    // Class 64, n <= 60: wave 0 sweeps the 64 lower 4 x 8 tiles of H, one per lane (tile
+    // L = lt_idx(br, bc)), with the full-tile pass's arithmetic: the pivot column K is
+    // assembled in LDS from column K of the tiles in tile column K / 8 (rows >= 8 (K / 8))
+    // and row K of the tiles in tile row K / 4 (columns < 8 (K / 8) + 8); the entries of
+    // the diagonal tiles above the diagonal ride along as the symmetric copies.  One wave:
+    // no workgroup barrier per pivot, and the four robots of a CU sweep on their wave 0,
+    // one per SIMD, instead of eight waves sharing the four SIMDs.  Wave 1 waits.
+    fsync<NT>();   // H's lower tiles are in LDS
+    if (wave == 0) {
+      int br = 0;
+#pragma unroll
+      for (int bb = 1; bb < 15; ++bb) br = lt_idx(bb, 0) <= lane ? bb : br;
+      const int bc = lane - lt_idx(br, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < TW; ++c) W[r][c] = sm.ht[(TW * r + c) * LANES + lane];
+      double* const zc = sm.zc[0];
+      double* const zc1 = sm.zc[1];
+      if (lane < 4) {   // rows 60..63: no tile holds them (padding)
+        zc[60 + lane] = 0.0;
+        zc1[60 + lane] = 0.0;
+      }
+#if MPCQP_C64_SYMPAIR
+      // pivot pairs {K, K + 1} (K even; K + 1 = n is the decoupled identity padding when n
+      // is odd), one rank-2 pass each as in classes 96 / 128: half the pivot chains
+#pragma unroll 1
+      for (int KT = 0; TW * KT < n; ++KT) {
+        static_for<TW / 2>([&](auto KPc) {
+          constexpr int KC = 2 * decltype(KPc)::value;
+          constexpr int KRR = KC & 3;   // 0 or 2
+          const int K = TW * KT + KC;
+          const int KR = 2 * KT + (KC >> 2);
+          if (K < n) {
+            if (br == KR) {   // rows K, K + 1: columns 8 bc .. 8 bc + 7
+              double r0[TW], r1[TW];
+#pragma unroll
+              for (int c = 0; c < TW; ++c) {
+                r0[c] = W[KRR][c];
+                r1[c] = W[KRR + 1][c];
+              }
+              stt<TW>(zc, bc, r0);
+              stt<TW>(zc1, bc, r1);
+            }
+            if (bc == KT) {   // columns K, K + 1: rows 4 br .. 4 br + 3 (written last)
+              d2* p0 = reinterpret_cast<d2*>(zc + 4 * br);
+              d2* p1 = reinterpret_cast<d2*>(zc1 + 4 * br);
+              p0[0] = d2{W[0][KC], W[1][KC]};
+              p0[1] = d2{W[2][KC], W[3][KC]};
+              p1[0] = d2{W[0][KC + 1], W[1][KC + 1]};
+              p1[1] = d2{W[2][KC + 1], W[3][KC + 1]};
+            }
+            fsync<LANES>();
+            double zr0[TW], zr1[TW], zi0[4], zi1[4];
+            ldt<TW>(zr0, zc, bc);
+            ldt<TW>(zr1, zc1, bc);
+            ld4(zi0, zc, br);
+            ld4(zi1, zc1, br);
+            const double d00 = zc[K], d01 = zc[K + 1], d11 = zc1[K + 1];
+            const double idet = rcp_nr(fma(d00, d11, -d01 * d01));
+            const double e00 = d11 * idet, e01 = -d01 * idet, e11 = d00 * idet;   // D^-1
+            double c0[4], c1[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              c0[r] = -fma(zi0[r], e00, zi1[r] * e01);
+              c1[r] = -fma(zi0[r], e01, zi1[r] * e11);
+            }
+            if (br == KR) {
+              c0[KRR] = e00 - 1.0;
+              c1[KRR] = e01;
+              c0[KRR + 1] = e01;
+              c1[KRR + 1] = e11 - 1.0;
+            }
+            if (bc == KT) {   // the pair's columns enter with D - I
+              zr0[KC] -= 1.0;
+              zr1[KC + 1] -= 1.0;
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+              for (int c = 0; c < TW; ++c) W[r][c] = fma(c1[r], zr1[c], fma(c0[r], zr0[c], W[r][c]));
+            if (bc == KT && br == KR) {
+              W[KRR][KC] -= 2.0;
+              W[KRR + 1][KC + 1] -= 2.0;
+            }
+            fsync<LANES>();   // every lane has read the pair's columns before the next are written
+          }
+        });
+      }
+#else
+#pragma unroll 1
+      for (int KT = 0; TW * KT < n; ++KT) {
+        static_for<TW>([&](auto KCc) {
+          constexpr int KC = decltype(KCc)::value;
+          constexpr int KRR = KC & 3;
+          const int K = TW * KT + KC;
+          const int KR = 2 * KT + (KC >> 2);
+          if (K < n) {
+            if (br == KR) {   // row K: columns 8 bc .. 8 bc + 7
+              double rowk[TW];
+#pragma unroll
+              for (int c = 0; c < TW; ++c) rowk[c] = W[KRR][c];
+              stt<TW>(zc, bc, rowk);
+            }
+            if (bc == KT) {   // column K: rows 4 br .. 4 br + 3 (written last: wins on the overlap)
+              d2* pz = reinterpret_cast<d2*>(zc + 4 * br);
+              pz[0] = d2{W[0][KC], W[1][KC]};
+              pz[1] = d2{W[2][KC], W[3][KC]};
+            }
+            fsync<LANES>();
+            double zr[TW], zi[4];
+            ldt<TW>(zr, zc, bc);
+            ld4(zi, zc, br);
+            const double dK = zc[K];
+            const double inv = rcp_nr(dK);
+            double beta[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) beta[r] = -zi[r] * inv;
+            if (br == KR) beta[KRR] = inv - 1.0;
+            if (bc == KT) zr[KC] = dK - 1.0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+              for (int c = 0; c < TW; ++c) W[r][c] = fma(beta[r], zr[c], W[r][c]);
+            W[KRR][KC] += (bc == KT && br == KR) ? -2.0 : 0.0;
+            fsync<LANES>();   // every lane has read the pivot column before the next is written
+          }
+        });
+      }
+#endif
+      // P = -(sweep result), staged in the second half of ht
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < TW; ++c) sm.ht[2048 + (TW * r + c) * LANES + lane] = -W[r][c];
+    }
+    fsync<NT>();
+    // every lane's full tile (tr, tc) of P: a lower tile directly, an upper one from the
+    // transposed entries of the lower tiles (2 tc + c / 4, tr / 2); rows / columns >= 60 are
+    // the padding's -identity
+    // the same for H (identity padding) back into the full lane-interleaved layout the
+    // drop path reads: its tile rows 2, 3 (full-layout elements 16..31: the staging half)
+    // once every lane holds its P tile, then rows 0, 1 (the lower-tile half)
+    {
+      const bool lower = tc <= (tr >> 1);
+      const int lb = lt_idx(tr < 15 ? tr : 14, tc);
+      const int ub0 = 256 * (tr & 1) + lt_idx(2 * tc, tr >> 1);
+      const int ub1 = 256 * (tr & 1) + lt_idx(2 * tc + 1 < 15 ? 2 * tc + 1 : 14, tr >> 1);
+      auto gaddr = [&](int r, int c) -> int {
+        return lower ? (TW * r + c) * LANES + lb : (TW * (c & 3) + r) * LANES + (c < 4 ? ub0 : ub1);
+      };
+      auto gvalid = [&](int r, int c) -> bool { return lower ? tr < 15 : (c < 4 || tc < 7); };
+      double Hh[2][TW];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < TW; ++c) {
+          const double v = sm.ht[2048 + gaddr(r, c)];
+          W[r][c] = gvalid(r, c) ? v : (4 * tr + r == TW * tc + c ? -1.0 : 0.0);
+        }
+#pragma unroll
+      for (int r = 2; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < TW; ++c) {
+          const double h = sm.ht[gaddr(r, c)];
+          Hh[r - 2][c] = gvalid(r, c) ? h : (4 * tr + r == TW * tc + c ? 1.0 : 0.0);
+        }
+      fsync<NT>();   // the staging half is read
+#pragma unroll
+      for (int r = 2; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < TW; ++c) sm.ht[(TW * r + c) * NT + tid] = Hh[r - 2][c];
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int c = 0; c < TW; ++c) {
+          const double h = sm.ht[gaddr(r, c)];
+          Hh[r][c] = gvalid(r, c) ? h : (4 * tr + r == TW * tc + c ? 1.0 : 0.0);
+        }
+      fsync<NT>();   // the lower-tile half is read
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int c = 0; c < TW; ++c) sm.ht[(TW * r + c) * NT + tid] = Hh[r][c];
+    }
+  } else if constexpr (kMfmaSweep) {
     // class 64: blocked by 4 pivots on the f64 matrix cores (mpcqp_sweep_mfma.h),
     // in the LDS of the H copy, which is stored afterwards
     double Ws[4][TW];
@@ -425,10 +635,12 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   }
   // P = -(sweep result) = H^-1 ; largest diagonal entry (dependency threshold scale)
   double wd = 0.0;
+  if constexpr (!kSym) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int c = 0; c < TW; ++c) W[r][c] = -W[r][c];
+      for (int c = 0; c < TW; ++c) W[r][c] = -W[r][c];
+  }
   if constexpr (TW == 8) {
     if (tc == (tr >> 1)) {
       // diagonal entries: column r (even tile row) or 4 + r (odd); blended
@@ -523,6 +735,17 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     u[k] = 0.0;
   }
   if (tid == 0) sm.choice = 0;   // no pass tag yet (MPCQP_SPLIT_CHOICE)
+  // the cone rows' coefficients (lanes 0..17: row r's a_i at 3 r + i) and dependency
+  // thresholds 1e-12 |a_r|^2 wscale (lanes 18..23) in one register, read by v_readlane into
+  // SGPRs when a row is chosen (an LDS load + readfirstlane chain otherwise)
+  constexpr bool kRowTab = NV <= 96;   // class 128: no VGPRs to spare (an 8-byte spill)
+  double rowtab = 0.0;
+  if (!kRowTab) {
+  } else if (lane < 18) rowtab = sm.mt.rows[lane / 3][lane % 3];
+  else if (lane < 24) {
+    const double* a = sm.mt.rows[lane - 18];
+    rowtab = 1e-12 * (a[0] * a[0] + a[1] * a[1] + a[2] * a[2]) * wscale;
+  }
   fsync<NT>();   // wb, vx and gv are dead: the loop reuses zc / vz / vr2
   unsigned long long occ[VPL];
 #pragma unroll
@@ -548,6 +771,54 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   int p = -1;                       // pending violated row (uniform)
   int v0 = 0, tcA = 0, c0 = 0;      // its foot-step's first variable, tile column, register column
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, thr = 0.0, sp = 0.0, up = 0.0;
+  // the next rows p (and its pair candidate p2): the most violated row in the dual metric
+  // (f32-rounded keys, lowest lane on ties), then the best row of any other foot-step;
+  // with the split choice (class 64) wave 1 publishes {p, p2} in one pass-tagged LDS word
+  constexpr bool kSplit = MPCQP_SPLIT_CHOICE && NV == 64 && C::NW == 2;
+  constexpr bool kEarly = kSplit && MPCQP_EARLY_CHOICE;
+  auto choose = [&](int tag_it, int& pc, int& pc2) {
+    pc = -1;
+    pc2 = -1;
+    double key[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k)
+      key[k] = s[k] < -tol ? s[k] * (double)(kCurKey ? __builtin_amdgcn_rsqf(fmaxf(qm[k], qfloor)) : qm[k]) : INFINITY;
+    double bv = key[0];
+    int bk = 0;
+#pragma unroll
+    for (int k = 1; k < CPL; ++k) {
+      bk = key[k] < bv ? k : bk;
+      bv = vmin(bv, key[k]);
+    }
+    double kmn;
+    const int pl = wave_argmin_f32(bv, kmn);
+    if (kmn < INFINITY) {
+      pc = pl + LANES * uni(__builtin_amdgcn_readlane(bk, pl));
+      if constexpr (SharedT<NV>::kPair) {
+        const int vc = 3 * (pc / 6);
+        double bw = INFINITY;
+        int bk2 = 0;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+          const double kk = cz[k] == vc ? INFINITY : key[k];
+          bk2 = kk < bw ? k : bk2;
+          bw = vmin(bw, kk);
+        }
+        double kmn2;
+        const int ql = wave_argmin_f32(bw, kmn2);
+        if (kmn2 < INFINITY) pc2 = ql + LANES * uni(__builtin_amdgcn_readlane(bk2, ql));
+      }
+    }
+    if constexpr (kSplit) {
+      if (lane == 0)
+        // relaxed workgroup-scope atomics, not volatile: a volatile access keeps the
+        // generic address space (a FLAT load / store with a vmcnt wait); these stay DS ops
+        __hip_atomic_store(&sm.choice, (((tag_it + 1) & 0xffff) << 16) | ((pc2 + 1) << 8) | (pc + 1),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  };
+  bool early = false;   // kEarly: wave 1 already holds (and has published) the next choice
+  int epc = -1, epc2 = -1;
   SEC(0);
   while (true) {
     // pair candidate p2 (another foot-step's most violated row), set on a fresh choice
@@ -561,45 +832,14 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       // pass-tagged LDS word, which wave 0 reads after its R update instead of
       // repeating both argmins (every decision is identical in both waves, so both
       // reach every choice point and every exit together).
-      constexpr bool kSplit = MPCQP_SPLIT_CHOICE && NV == 64 && C::NW == 2;
       int pc = -1, pc2 = -1;
       if (!kSplit || wave == 1) {
-        double key[CPL];
-#pragma unroll
-        for (int k = 0; k < CPL; ++k)
-          key[k] = s[k] < -tol ? s[k] * (double)(kCurKey ? __builtin_amdgcn_rsqf(fmaxf(qm[k], qfloor)) : qm[k]) : INFINITY;
-        double bv = key[0];
-        int bk = 0;
-#pragma unroll
-        for (int k = 1; k < CPL; ++k) {
-          bk = key[k] < bv ? k : bk;
-          bv = vmin(bv, key[k]);
-        }
-        double kmn;
-        const int pl = wave_argmin_f32(bv, kmn);
-        if (kmn < INFINITY) {
-          pc = pl + LANES * uni(__builtin_amdgcn_readlane(bk, pl));
-          if constexpr (SharedT<NV>::kPair) {
-            const int vc = 3 * (pc / 6);
-            double bw = INFINITY;
-            int bk2 = 0;
-#pragma unroll
-            for (int k = 0; k < CPL; ++k) {
-              const double kk = cz[k] == vc ? INFINITY : key[k];
-              bk2 = kk < bw ? k : bk2;
-              bw = vmin(bw, kk);
-            }
-            double kmn2;
-            const int ql = wave_argmin_f32(bw, kmn2);
-            if (kmn2 < INFINITY) pc2 = ql + LANES * uni(__builtin_amdgcn_readlane(bk2, ql));
-          }
-        }
-        if constexpr (kSplit) {
-          if (lane == 0)
-            // relaxed workgroup-scope atomics, not volatile: a volatile access keeps the
-            // generic address space (a FLAT load / store with a vmcnt wait); these stay DS ops
-            __hip_atomic_store(&sm.choice, (((it + 1) & 0xffff) << 16) | ((pc2 + 1) << 8) | (pc + 1),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (kEarly && early) {   // chosen (and published) at the end of the previous pass
+          pc = epc;
+          pc2 = epc2;
+          early = false;
+        } else {
+          choose(it, pc, pc2);
         }
       } else {
         const int tag = (it + 1) & 0xffff;
@@ -619,10 +859,17 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       const double vmn = readlane_d(sv, pl);
       CNT(4);
       const int rp = p % 6;
-      a0 = sgpr_d(sm.mt.rows[rp][0]);
-      a1 = sgpr_d(sm.mt.rows[rp][1]);
-      a2 = sgpr_d(sm.mt.rows[rp][2]);
-      thr = sgpr_d(1e-12 * (a0 * a0 + a1 * a1 + a2 * a2) * wscale);
+      if constexpr (kRowTab) {
+        a0 = readlane_d(rowtab, 3 * rp);
+        a1 = readlane_d(rowtab, 3 * rp + 1);
+        a2 = readlane_d(rowtab, 3 * rp + 2);
+        thr = readlane_d(rowtab, 18 + rp);
+      } else {
+        a0 = sgpr_d(sm.mt.rows[rp][0]);
+        a1 = sgpr_d(sm.mt.rows[rp][1]);
+        a2 = sgpr_d(sm.mt.rows[rp][2]);
+        thr = sgpr_d(1e-12 * (a0 * a0 + a1 * a1 + a2 * a2) * wscale);
+      }
       v0 = 3 * (p / 6);
       tcA = (int)((unsigned)v0 / TW);   // v0 >= 0: shifts for TW = 8
       c0 = (int)((unsigned)v0 % TW);
@@ -637,10 +884,17 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         sp2 = sgpr_d(readlane_d(sv2, ql));
         p2 = pc2;
         const int rq = p2 % 6;
-        b0 = sgpr_d(sm.mt.rows[rq][0]);
-        b1 = sgpr_d(sm.mt.rows[rq][1]);
-        b2 = sgpr_d(sm.mt.rows[rq][2]);
-        thr2 = sgpr_d(1e-12 * (b0 * b0 + b1 * b1 + b2 * b2) * wscale);
+        if constexpr (kRowTab) {
+          b0 = readlane_d(rowtab, 3 * rq);
+          b1 = readlane_d(rowtab, 3 * rq + 1);
+          b2 = readlane_d(rowtab, 3 * rq + 2);
+          thr2 = readlane_d(rowtab, 18 + rq);
+        } else {
+          b0 = sgpr_d(sm.mt.rows[rq][0]);
+          b1 = sgpr_d(sm.mt.rows[rq][1]);
+          b2 = sgpr_d(sm.mt.rows[rq][2]);
+          thr2 = sgpr_d(1e-12 * (b0 * b0 + b1 * b1 + b2 * b2) * wscale);
+        }
         const int w0 = 3 * (p2 / 6);
         tcA2 = (int)((unsigned)w0 / TW);   // w0 >= 0: shifts for TW = 8
         c02 = (int)((unsigned)w0 % TW);
@@ -790,11 +1044,19 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
           for (int k = 0; k < CPL; ++k)
             qm[k] = (float)((double)qm[k] - fma(i11 * zs[k], zs[k], fma(2.0 * i12 * zs[k], zs2[k], i22 * zs2[k] * zs2[k])));
+        ++it;   // a pair step counts as the two additions it makes
+        if constexpr (kEarly) {
+          if (wave == 1) {   // the row values are final for this pass: choose now, before the FMAs
+            choose(it, epc, epc2);
+            early = true;
+          }
+        }
         double cz1[TW], cz2[TW], z41[4], z42[4];
         ldt<TW>(cz1, vz, tc);
         ldt<TW>(cz2, vz2, tc);
         ld4(z41, vz, tr);
         ld4(z42, vz2, tr);
+#ifndef MPCQP_ABL_NOUPD
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const double al = fma(i11, z41[r], i12 * z42[r]);
@@ -817,9 +1079,9 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
             for (int c = 0; c < TW; ++c) Rm[r][c] = fma(-be, cz2[c], fma(-al, cz1[c], Rm[r][c]));
           }
         }
+#endif
         p = -1;
         CNT(15);
-        ++it;   // a pair step counts as the two additions it makes
         SEC(0);
         continue;
       }
@@ -890,6 +1152,12 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
       for (int k = 0; k < CPL; ++k) s[k] = (lane + LANES * k == p) ? 0.0 : s[k];
       p = -1;
+      if constexpr (kEarly) {
+        if (wave == 1) {   // the row values are final for this pass: choose before the FMAs
+          choose(it, epc, epc2);
+          early = true;
+        }
+      }
     } else {
       // drop slot l: eta = Minv_ll, y = Minv[:, l] = R (H R_l^T)
       const int lt = l >> 2, lr = l & 3;
@@ -940,6 +1208,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       occ[l >> 6] &= ~(1ull << (l & 63));
     }
     SEC(13);
+#ifndef MPCQP_ABL_NOUPD
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -950,6 +1219,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
         for (int c = 0; c < TW; ++c) Rm[r][c] = fma(aR[r], cv[c], Rm[r][c]);
     }
+#endif
     if (zrow >= 0) {
       if constexpr (kCurKey) {
 #pragma unroll
@@ -1003,6 +1273,10 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   if (tid == 0 && Ug) {
     unsigned long long* dst = (unsigned long long*)(Ug + (size_t)b * N * 12);
     for (int i = 0; i < 7; ++i) dst[i] = stamps_[i];
+    if (N * 6 > 45) {
+      dst[44] = rt0_;
+      dst[45] = __builtin_amdgcn_s_memrealtime();
+    }
   }
   fsync<NT>();
   if (lane < 16 && Ug && 26 + 16 * (NT / LANES - 1) < N * 6) {   // per-wave section accumulators
@@ -1011,7 +1285,9 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   }
   if (lane == 0 && Ug && 24 + wave < N * 6) {   // HW_ID of each wave (SIMD, CU, SE)
     unsigned long long* dst = (unsigned long long*)(Ug + (size_t)b * N * 12);
-    dst[24 + wave] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    dst[24 + wave] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                     ((unsigned long long)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15) << 32) |
+                     ((unsigned long long)blockIdx.x << 40);   // + XCC_ID, workgroup id
   }
   Ug = nullptr;
 #endif

@@ -19,11 +19,8 @@ from mpcqp.synthetic import make_batch  # noqa: E402
 PHASES = ["inputs, model, Ya/Yb, g", "H tile", "sweep H^-1", "active set", "KKT check", "-"]
 
 
-def main():
-    B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
-    N = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-    gaits = tuple(sys.argv[3].split(",")) if len(sys.argv) > 3 else ("trot10",)
-    seed = int(sys.argv[4]) if len(sys.argv) > 4 else 1000
+def run_raw(B, N, gaits, seed, with_iters=False):
+    """Run the stamps build once (3 launches) and return U as a NumPy array."""
     _lib.LIB_PATH = os.environ.get("MPCQP_STAMPS_LIB") or os.path.join(ROOT, "pympc-quadruped_amd", "mpcqp",
                                                                        "libmpcqp_stamps.so")
     lib = _lib.load()
@@ -42,21 +39,38 @@ def main():
         lib.mpcqp_solve(ctx, B, P(d["x0"]), P(d["xref"]), P(d["contact"]), P(d["feet"]), P(d["robot"]),
                         P(u0), P(U), P(st), P(it), ctypes.c_void_p(0))
     torch.cuda.synchronize()
-    ts = U.cpu().numpy().reshape(B, -1).view(np.uint64)[:, :7].astype(np.int64)
+    if with_iters:
+        return U.cpu().numpy(), it.cpu().numpy()
+    return U.cpu().numpy()
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+    N = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    gaits = tuple(sys.argv[3].split(",")) if len(sys.argv) > 3 else ("trot10",)
+    seed = int(sys.argv[4]) if len(sys.argv) > 4 else 1000
+    Un, iters = run_raw(B, N, gaits, seed, with_iters=True)
+    ts = Un.reshape(B, -1).view(np.uint64)[:, :7].astype(np.int64)
     dts = np.diff(ts, axis=1)
-    iters = it.cpu().numpy()
     print(f"B={B} N={N}  iterations mean {iters.mean():.1f} max {iters.max()}")
     for k, name in enumerate(PHASES):
         print(f"  {name:26s} median {np.median(dts[:, k]):9.0f}  max {dts[:, k].max():9.0f} cycles")
     tot = ts[:, 6] - ts[:, 0]
     print(f"  {'total':26s} median {np.median(tot):9.0f}  max {tot.max():9.0f}")
+    # start / end over the whole launch (s_memrealtime: 100 MHz, chip-wide): dispatch ramp and tail
+    rt = Un.reshape(B, -1).view(np.uint64)[:, 44:46].astype(np.int64)
+    if rt[:, 0].min() > 0:
+        t0 = (rt[:, 0] - rt[:, 0].min()) * 0.01
+        t1 = (rt[:, 1] - rt[:, 0].min()) * 0.01
+        print(f"  robot start (us after the first): median {np.median(t0):.2f} p90 {np.percentile(t0, 90):.2f} "
+              f"max {t0.max():.2f}; end median {np.median(t1):.2f} p90 {np.percentile(t1, 90):.2f} max {t1.max():.2f}")
     for i in np.argsort(tot)[-4:]:
         print(f"  slow robot {i}: total {tot[i]} iterations {iters[i]} phases {dts[i, :5].tolist()}")
     gi = dts[:, 3]
     sel = iters > 0
     print(f"  active-set cycles / iteration: median {np.median(gi[sel] / iters[sel]):.0f}")
-    sec = U.cpu().numpy().reshape(B, -1).view(np.uint64)[:, 8:24].astype(np.int64)
-    sec1 = U.cpu().numpy().reshape(B, -1).view(np.uint64)[:, 26:42].astype(np.int64)
+    sec = Un.reshape(B, -1).view(np.uint64)[:, 8:24].astype(np.int64)
+    sec1 = Un.reshape(B, -1).view(np.uint64)[:, 26:42].astype(np.int64)
     # section k runs from SEC(k) to the next SEC (mpcqp_solve.h)
     names = ["argmin p + a_p rows", "combo + LDS store", "zs = A z (LDS)", "-", "-", "add: q, 1/s, loads, coefs",
              "drop: R_l, H R_l, R H R_l", "-", "pair candidate", "barrier", "pair-step test",
@@ -65,7 +79,7 @@ def main():
     cnt = {"pair tests": sec[:, 3], "fresh choices": sec[:, 4], "drops": sec[:, 14], "pair steps": sec[:, 15]}
     for k, v in cnt.items():
         print(f"  count {k:14s} mean {v[sel].mean():6.1f}  max {v.max():4d}")
-    hw = U.cpu().numpy().reshape(B, -1).view(np.uint64)[:, 24:26].astype(np.int64)
+    hw = Un.reshape(B, -1).view(np.uint64)[:, 24:26].astype(np.int64)
     simd = (hw >> 4) & 3
     cu = ((hw >> 8) & 15) | (((hw >> 13) & 7) << 4)
     print(f"  waves 0/1 on the same SIMD: {(simd[:, 0] == simd[:, 1]).mean():.3f}  same CU: "
