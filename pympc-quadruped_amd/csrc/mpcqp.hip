@@ -63,6 +63,14 @@ static_assert(kMaxN == 20, "the dense classes' and the interior-point class's LD
 // (no barrier per pivot, half the VALU of the two-wave sweep); n = 61..64 go to class 96
 #define MPCQP_C64_SYMSWEEP 0   // measured slower: off
 #endif
+#ifndef MPCQP_ASM_COMBO
+// class 64's z / r column combination as one computed jump (mpcqp_combo_asm.h) instead of
+// the compiler's branch tree over an 8-way switch
+#define MPCQP_ASM_COMBO 1
+#endif
+#ifndef MPCQP_DUP
+#define MPCQP_DUP 0   // diagnostic builds only: duplicate one loop component (tools/gpu_ab.sh pricing)
+#endif
 #ifndef MPCQP_EARLY_CHOICE
 // class 64 split choice: wave 1 chooses the next rows as soon as the pass has updated the
 // row values, before its rank-1 / rank-2 FMAs, so wave 0 finds the choice published
@@ -321,6 +329,7 @@ __device__ __forceinline__ int wave_argmin_f32(double v, double& vmin_out) {
 
 #include "mpcqp_form.h"
 #include "mpcqp_sweep_mfma.h"
+#include "mpcqp_combo_asm.h"
 #include "mpcqp_solve.h"
 #include "mpcqp_ipm.h"
 #include "mpcqp_plan.h"

@@ -776,7 +776,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   // with the split choice (class 64) wave 1 publishes {p, p2} in one pass-tagged LDS word
   constexpr bool kSplit = MPCQP_SPLIT_CHOICE && NV == 64 && C::NW == 2;
   constexpr bool kEarly = kSplit && MPCQP_EARLY_CHOICE;
-  auto choose = [&](int tag_it, int& pc, int& pc2) {
+  auto choose1 = [&](int tag_it, int& pc, int& pc2) {
     pc = -1;
     pc2 = -1;
     double key[CPL];
@@ -816,6 +816,15 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         __hip_atomic_store(&sm.choice, (((tag_it + 1) & 0xffff) << 16) | ((pc2 + 1) << 8) | (pc + 1),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+  };
+  auto choose = [&](int tag_it, int& pc, int& pc2) {
+    choose1(tag_it, pc, pc2);
+#if MPCQP_DUP == 2   // diagnostic: the choice twice (same result), to price it on the critical path
+    int qq, qq2;
+    choose1(tag_it, qq, qq2);
+    pc = (qq == pc) ? pc : -1;
+    pc2 = (qq2 == pc2) ? pc2 : -1;
+#endif
   };
   bool early = false;   // kEarly: wave 1 already holds (and has published) the next choice
   int epc = -1, epc2 = -1;
@@ -910,6 +919,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     const bool rlive = slots_live(RPW * wave);
     // rows 4tr..4tr+3 of P a and R a for a row a of the foot-step at variable
     // 8 tA + cA, stored by the lanes of tile column tA
+    constexpr bool kAsmCombo = NV == 64 && TW == 8 && MPCQP_ASM_COMBO;
     auto combo_store = [&](int cA, int tA, double e0, double e1, double e2, double* dz, double* dr) {
       double zq[4], rq[4];
       if constexpr (TW == 6) {   // foot-steps start at register column 0 or 3: never straddle
@@ -922,6 +932,12 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
           case 2: colcombo<2, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
           default: colcombo<3, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
         }
+      } else if constexpr (kAsmCombo) {
+        // one computed jump into eight straight-line cases (mpcqp_combo_asm.h), the
+        // coefficients masked by the tile column each of the three columns lies in; R's
+        // half unconditionally (rows of no active slot are zero)
+        const int t1 = tA + (cA == 7 ? 1 : 0), t2 = tA + (cA >= 6 ? 1 : 0);
+        combo_asm64(W, Rm, cA, tc == tA ? e0 : 0.0, tc == t1 ? e1 : 0.0, tc == t2 ? e2 : 0.0, zq, rq);
       } else {
         switch (cA) {
           case 0: colcombo<0, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
@@ -934,7 +950,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
           default: colcombo<7, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
         }
       }
-      if (TW != 6 && cA + 2 >= TW) {   // the foot-step straddles tile columns tA, tA + 1 (next lane)
+      if (TW != 6 && __builtin_expect(cA + 2 >= TW, 0)) {   // the foot-step straddles tile columns tA, tA + 1
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           zq[r] += dpp_shl1(zq[r]);
@@ -953,8 +969,19 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     double* const vr2 = sm.vr2[buf];
     combo_store(c0, tcA, a0, a1, a2, vz, vr);
     if (p2 >= 0) combo_store(c02, tcA2, b0, b1, b2, vz2, vr2);
+#if MPCQP_DUP == 1   // diagnostic: the combos twice (same values), to price them on the critical path
+    {
+      double oz = 0.0;
+      asm volatile("" : "+v"(oz));
+      combo_store(c0, tcA, a0 + oz, a1, a2, vz, vr);
+      if (p2 >= 0) combo_store(c02, tcA2, b0 + oz, b1, b2, vz2, vr2);
+    }
+#endif
     SEC(9);
     fsync<NT>();
+#if MPCQP_DUP == 3   // diagnostic: one more workgroup barrier per pass
+    fsync<NT>();
+#endif
     SEC(2);
     // constraint-row steps zs = A z, slot directions r, variable steps
     double zs[CPL];
@@ -1004,6 +1031,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         bad |= mine && fma(-tq, rs2[k], fma(-tp, rs1[k], u[k])) < 0.0;
       }
       if (ok && !__any(bad)) {
+        SEC(16);
 #pragma unroll
         for (int k = 0; k < VPL; ++k) {
           const double zx1 = vz[lane + LANES * k], zx2 = vz2[lane + LANES * k];
@@ -1051,6 +1079,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
             early = true;
           }
         }
+        SEC(17);
         double cz1[TW], cz2[TW], z41[4], z42[4];
         ldt<TW>(cz1, vz, tc);
         ldt<TW>(cz2, vz2, tc);
@@ -1064,6 +1093,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
           for (int c = 0; c < TW; ++c) W[r][c] = fma(-be, cz2[c], fma(-al, cz1[c], W[r][c]));
         }
+        SEC(18);
         if (rlive || slots_live(RPW * wave)) {
           // r / r2 entries read per row (not as two 4-vectors): the shorter live
           // ranges keep the kernel spill-free (a 4-byte VGPR spill here otherwise,
@@ -1282,6 +1312,10 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   if (lane < 16 && Ug && 26 + 16 * (NT / LANES - 1) < N * 6) {   // per-wave section accumulators
     unsigned long long* dst = (unsigned long long*)(Ug + (size_t)b * N * 12);
     dst[(wave == 0 ? 8 : 10 + 16 * wave) + lane] = secacc_;
+  }
+  if (lane >= 16 && lane < 19 && Ug && NT == 128 && N * 6 >= 52) {   // sections 16..18 (pair step split)
+    unsigned long long* dst = (unsigned long long*)(Ug + (size_t)b * N * 12);
+    dst[46 + 3 * wave + (lane - 16)] = secacc_;
   }
   if (lane == 0 && Ug && 24 + wave < N * 6) {   // HW_ID of each wave (SIMD, CU, SE)
     unsigned long long* dst = (unsigned long long*)(Ug + (size_t)b * N * 12);

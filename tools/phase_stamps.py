@@ -89,6 +89,11 @@ def main():
         print(f"  robot {i}: it {iters[i]} fresh {sec[i, 4]} pair tests {sec[i, 3]} pairs {sec[i, 15]} "
               f"drops {sec[i, 14]} loop cycles {dts[i, 3]} per pass {dts[i, 3] / max(1, iters[i] - sec[i, 15]):.0f}")
         print("     sections:", {names[k]: int(sec[i, k]) for k in range(16) if names[k] != "-"})
+        ex = Un.reshape(B, -1).view(np.uint64)[i, 46:52].astype(np.int64)
+        if ex.any():
+            print("     pair step split (wave 0 / wave 1): decision (sec 10)", int(sec[i, 10]), int(sec1[i, 10]),
+                  "| accept bookkeeping", int(ex[0]), int(ex[3]), "| W rank-2", int(ex[1]), int(ex[4]),
+                  "| R rank-2", int(ex[2]), int(ex[5]))
         print("     wave 1:  ", {names[k]: int(sec1[i, k]) for k in range(16) if names[k] != "-"})
     tot_it = iters[sel].sum()
     for k, name in enumerate(names):
