@@ -68,6 +68,9 @@ static_assert(kMaxN == 20, "the dense classes' and the interior-point class's LD
 // the compiler's branch tree over an 8-way switch
 #define MPCQP_ASM_COMBO 1
 #endif
+#ifndef MPCQP_SLOT_COEF
+#define MPCQP_SLOT_COEF 1   // class 64: pair steps' R row coefficients computed once per slot lane
+#endif
 #ifndef MPCQP_DUP
 #define MPCQP_DUP 0   // diagnostic builds only: duplicate one loop component (tools/gpu_ab.sh pricing)
 #endif
@@ -282,15 +285,23 @@ __device__ __forceinline__ void st4(double* base, int k, const double (&v)[4]) {
 // monotone, so the f64 minimum's f32 image is the f32 minimum: a unique f32
 // minimum IS the exact answer; f32 ties fall back to the f64 reduction.  The
 // f32 reduction is one DPP-encoded v_min_f32 per stage.
-#define MPCQP_MIN_F32_DPP(ctrl) \
-  asm volatile("s_nop 1\n\tv_min_f32_dpp %0, %0, %0 " ctrl : "+v"(v))
+// The six stages are one asm statement: each DPP read of the previous stage's VGPR needs
+// two wait states (s_nop 1), and separate statements made hipcc pad every boundary again.
 __device__ __forceinline__ float wave_min_f32(float v) {
-  MPCQP_MIN_F32_DPP("quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf");
-  MPCQP_MIN_F32_DPP("quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf");
-  MPCQP_MIN_F32_DPP("row_half_mirror row_mask:0xf bank_mask:0xf");
-  MPCQP_MIN_F32_DPP("row_mirror row_mask:0xf bank_mask:0xf");
-  MPCQP_MIN_F32_DPP("row_bcast:15 row_mask:0xa bank_mask:0xf");
-  MPCQP_MIN_F32_DPP("row_bcast:31 row_mask:0xc bank_mask:0xf");
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_min_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+      : "+v"(v));
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 // lowest lane holding the wave minimum of v (+inf = no candidate); vmin_out = that minimum

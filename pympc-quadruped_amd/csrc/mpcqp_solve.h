@@ -1065,9 +1065,20 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         }
         occ[qa >> 6] |= 1ull << (qa & 63);
         occ[qb >> 6] |= 1ull << (qb & 63);
+        // class 64: R's row coefficients -(al, be) once per slot lane (both waves write the
+        // same values), read back by tile row below -- instead of per tile row, with two
+        // LDS loads and two selects each (tv / yv are written only on drop passes, after
+        // the next pass's barrier)
+        constexpr bool kSlotCoef = NV == 64 && VPL == 1 && MPCQP_SLOT_COEF;
+        const double i11 = s22 * id, i12 = -s12 * id, i22 = zsp * id;
+        if constexpr (kSlotCoef) {
+          const double e1 = rs1[0] - (lane == qa ? 1.0 : 0.0);
+          const double e2 = rs2[0] - (lane == qb ? 1.0 : 0.0);
+          sm.tv[lane] = -fma(i11, e1, i12 * e2);
+          sm.yv[lane] = -fma(i12, e1, i22 * e2);
+        }
         // rank-2 updates: row coefficients (al, be) = S^-1 (row's pair), then
         // M[r][c] -= al cz1[c] + be cz2[c]
-        const double i11 = s22 * id, i12 = -s12 * id, i22 = zsp * id;
         if constexpr (kCurKey)
 #pragma unroll
           for (int k = 0; k < CPL; ++k)
@@ -1098,6 +1109,16 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
           // r / r2 entries read per row (not as two 4-vectors): the shorter live
           // ranges keep the kernel spill-free (a 4-byte VGPR spill here otherwise,
           // written back as ~266 KiB of scratch per config-2 launch)
+          if constexpr (kSlotCoef) {
+            fsync<LANES>();   // this wave's tv / yv stores are done
+            double nal[4], nbe[4];
+            ld4(nal, sm.tv, tr);
+            ld4(nbe, sm.yv, tr);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+              for (int c = 0; c < TW; ++c) Rm[r][c] = fma(nbe[r], cz2[c], fma(nal[r], cz1[c], Rm[r][c]));
+          } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int sl = 4 * tr + r;
@@ -1107,6 +1128,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
             const double be = fma(i12, e1, i22 * e2);
 #pragma unroll
             for (int c = 0; c < TW; ++c) Rm[r][c] = fma(-be, cz2[c], fma(-al, cz1[c], Rm[r][c]));
+          }
           }
         }
 #endif
@@ -1168,13 +1190,19 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
         for (int k = 0; k < CPL; ++k) qm[k] = (float)fma(-zs[k] * zs[k], is, (double)qm[k]);
       double zr4[4], rr4[4];
+      constexpr bool kSlotCoef1 = NV == 64 && VPL == 1 && MPCQP_SLOT_COEF;
+      if constexpr (kSlotCoef1) {   // R's row coefficient once per slot lane (as the pair step's)
+        sm.tv[lane] = ((lane == q) ? 1.0 - rs[0] : -rs[0]) * is;
+        fsync<LANES>();
+      }
       ld4(zr4, vz, tr);
       ldt<TW>(cv, vz, tc);
-      ld4(rr4, vr, tr);
+      ld4(rr4, kSlotCoef1 ? sm.tv : vr, tr);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         aW[r] = -zr4[r] * is;
-        aR[r] = ((4 * tr + r == q) ? 1.0 - rr4[r] : -rr4[r]) * is;
+        if constexpr (kSlotCoef1) aR[r] = rr4[r];
+        else aR[r] = ((4 * tr + r == q) ? 1.0 - rr4[r] : -rr4[r]) * is;
       }
 #pragma unroll
       for (int k = 0; k < VPL; ++k) u[k] = (lane + LANES * k == q) ? up : u[k];
