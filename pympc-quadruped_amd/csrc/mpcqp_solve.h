@@ -935,7 +935,8 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       } else if constexpr (kAsmCombo) {
         // one computed jump into eight straight-line cases (mpcqp_combo_asm.h), the
         // coefficients masked by the tile column each of the three columns lies in; R's
-        // half unconditionally (rows of no active slot are zero)
+        // half unconditionally (rows of no active slot are zero; a second, P-only table
+        // for those waves measured 0.6 % slower)
         const int t1 = tA + (cA == 7 ? 1 : 0), t2 = tA + (cA >= 6 ? 1 : 0);
         combo_asm64(W, Rm, cA, tc == tA ? e0 : 0.0, tc == t1 ? e1 : 0.0, tc == t2 ? e2 : 0.0, zq, rq);
       } else {
@@ -987,6 +988,14 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     double zs[CPL];
 #pragma unroll
     for (int k = 0; k < CPL; ++k) zs[k] = cdot(vz, k);
+#if MPCQP_DUP == 5   // diagnostic: the constraint-row products once more (same values)
+    {
+      double oz = 0.0;
+      asm volatile("" : "+v"(oz));
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) zs[k] = cdot(vz, k) + oz * zs[k];
+    }
+#endif
     double zsp = zs[0];
 #pragma unroll
     for (int k = 1; k < CPL; ++k) zsp = (k == (p >> 6)) ? zs[k] : zsp;
@@ -1104,6 +1113,16 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
           for (int c = 0; c < TW; ++c) W[r][c] = fma(-be, cz2[c], fma(-al, cz1[c], W[r][c]));
         }
+#if MPCQP_DUP == 6   // diagnostic: P's rank-2 FMAs once more with opaque zero coefficients
+        {
+          double oz = 0.0;
+          asm volatile("" : "+v"(oz));
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < TW; ++c) W[r][c] = fma(oz, cz2[c], fma(oz, cz1[c], W[r][c]));
+        }
+#endif
         SEC(18);
         if (rlive || slots_live(RPW * wave)) {
           // r / r2 entries read per row (not as two 4-vectors): the shorter live
@@ -1118,6 +1137,16 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
             for (int r = 0; r < 4; ++r)
 #pragma unroll
               for (int c = 0; c < TW; ++c) Rm[r][c] = fma(nbe[r], cz2[c], fma(nal[r], cz1[c], Rm[r][c]));
+#if MPCQP_DUP == 7   // diagnostic: R's rank-2 FMAs once more with opaque zero coefficients
+            {
+              double oz = 0.0;
+              asm volatile("" : "+v"(oz));
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int c = 0; c < TW; ++c) Rm[r][c] = fma(oz, cz2[c], fma(oz, cz1[c], Rm[r][c]));
+            }
+#endif
           } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
