@@ -11,7 +11,7 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT" "$OUT/summary"
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- \
-  python3 bench.py --no-cpu --steps 20 --warmup 3 "$@" > "$OUT/bench_kt.json"
+  python3 bench.py --no-cpu --no-hint-line --steps 20 --warmup 3 "$@" > "$OUT/bench_kt.json"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o pmc --output-format csv -- \
   python3 bench.py --no-cpu --steps 5 --warmup 1 "$@" > "$OUT/bench_fetch.json"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o pmc --output-format csv -- \
