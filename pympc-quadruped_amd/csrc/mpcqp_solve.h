@@ -933,12 +933,23 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
           default: colcombo<3, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
         }
       } else if constexpr (kAsmCombo) {
-        // one computed jump into eight straight-line cases (mpcqp_combo_asm.h), the
-        // coefficients masked by the tile column each of the three columns lies in; R's
-        // half unconditionally (rows of no active slot are zero; a second, P-only table
-        // for those waves measured 0.6 % slower)
-        const int t1 = tA + (cA == 7 ? 1 : 0), t2 = tA + (cA >= 6 ? 1 : 0);
-        combo_asm64(W, Rm, cA, tc == tA ? e0 : 0.0, tc == t1 ? e1 : 0.0, tc == t2 ? e2 : 0.0, zq, rq);
+        // one computed jump into straight-line cases (mpcqp_combo_asm.h); R's half
+        // unconditionally (rows of no active slot are zero; a second, P-only table for those
+        // waves measured 0.6 % slower).  A foot-step inside one tile column (c0 <= 5) takes
+        // the SGPR coefficients unmasked -- only that tile column's lanes store; a straddling
+        // one masks them by the tile column each of its three columns lies in and adds the
+        // next lane's partial.
+        if (__builtin_expect(cA + 2 >= TW, 0)) {
+          const int t1 = tA + (cA == 7 ? 1 : 0), t2 = tA + (cA >= 6 ? 1 : 0);
+          combo_asm64(W, Rm, cA, tc == tA ? e0 : 0.0, tc == t1 ? e1 : 0.0, tc == t2 ? e2 : 0.0, zq, rq);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            zq[r] += dpp_shl1(zq[r]);
+            rq[r] += dpp_shl1(rq[r]);
+          }
+        } else {
+          combo_asm64_s(W, Rm, cA, e0, e1, e2, zq, rq);
+        }
       } else {
         switch (cA) {
           case 0: colcombo<0, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
@@ -951,7 +962,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
           default: colcombo<7, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
         }
       }
-      if (TW != 6 && __builtin_expect(cA + 2 >= TW, 0)) {   // the foot-step straddles tile columns tA, tA + 1
+      if (TW != 6 && !kAsmCombo && __builtin_expect(cA + 2 >= TW, 0)) {   // straddles tile columns tA, tA + 1
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           zq[r] += dpp_shl1(zq[r]);
