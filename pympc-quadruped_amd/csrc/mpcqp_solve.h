@@ -166,6 +166,22 @@ __device__ __forceinline__ void colcombo(const double (&Pm)[4][TW], const double
   }
 }
 
+// colcombo without the per-lane tile-column mask (uniform coefficients): for foot-steps
+// that lie inside one tile column, whose lanes alone store the result
+template <int C0, int TW>
+__device__ __forceinline__ void colcombo_u(const double (&Pm)[4][TW], const double (&Rm)[4][TW], double a0, double a1,
+                                           double a2, bool rlive, double (&zq)[4], double (&rq)[4]) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) zq[r] = fma(a2, Pm[r][C0 + 2], fma(a1, Pm[r][C0 + 1], a0 * Pm[r][C0]));
+  if (rlive) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rq[r] = fma(a2, Rm[r][C0 + 2], fma(a1, Rm[r][C0 + 1], a0 * Rm[r][C0]));
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rq[r] = 0.0;
+  }
+}
+
 template <int NT>
 __device__ __forceinline__ void write_empty_t(int b, int tid, int N, int code, float* u0g, float* Ug, int* statusg,
                                               int* itersg) {
@@ -919,12 +935,13 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     const bool rlive = slots_live(RPW * wave);
     // rows 4tr..4tr+3 of P a and R a for a row a of the foot-step at variable
     // 8 tA + cA, stored by the lanes of tile column tA
-    constexpr bool kAsmCombo = NV == 64 && TW == 8 && MPCQP_ASM_COMBO;
+    constexpr bool kAsmCombo = (NV == 64 || NV == 128) && TW == 8 && MPCQP_ASM_COMBO;
     auto combo_store = [&](int cA, int tA, double e0, double e1, double e2, double* dz, double* dr) {
       double zq[4], rq[4];
-      if constexpr (TW == 6) {   // foot-steps start at register column 0 or 3: never straddle
-        if (cA == 0) colcombo<0, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq);
-        else colcombo<3, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq);
+      if constexpr (TW == 6) {   // foot-steps start at register column 0 or 3: never straddle,
+        // so the uniform (SGPR) coefficients need no per-lane mask: only tile column tA stores
+        if (cA == 0) colcombo_u<0, TW>(W, Rm, e0, e1, e2, rlive, zq, rq);
+        else colcombo_u<3, TW>(W, Rm, e0, e1, e2, rlive, zq, rq);
       } else if constexpr (TW == 4) {
         switch (cA) {
           case 0: colcombo<0, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
