@@ -71,6 +71,9 @@ static_assert(kMaxN == 20, "the dense classes' and the interior-point class's LD
 #ifndef MPCQP_SLOT_COEF
 #define MPCQP_SLOT_COEF 1   // class 64: pair steps' R row coefficients computed once per slot lane
 #endif
+#ifndef MPCQP_F32_KEY
+#define MPCQP_F32_KEY 1   // row keys in f32 throughout (not bitwise identical to f64 keys: near-ties may resolve differently)
+#endif
 #ifndef MPCQP_DUP
 #define MPCQP_DUP 0   // diagnostic builds only: duplicate one loop component (tools/gpu_ab.sh pricing)
 #endif

@@ -795,6 +795,48 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   auto choose1 = [&](int tag_it, int& pc, int& pc2) {
     pc = -1;
     pc2 = -1;
+#if MPCQP_F32_KEY
+    if constexpr (kCurKey) {   // the keys in f32 throughout: the argmin is an f32 selection anyway
+      float keyf[CPL];
+#pragma unroll
+      for (int k = 0; k < CPL; ++k)
+        keyf[k] = s[k] < -tol ? (float)s[k] * __builtin_amdgcn_rsqf(fmaxf(qm[k], qfloor)) : INFINITY;
+      float bv = keyf[0];
+      int bk = 0;
+#pragma unroll
+      for (int k = 1; k < CPL; ++k) {
+        bk = keyf[k] < bv ? k : bk;
+        bv = fminf(bv, keyf[k]);
+      }
+      const float fm = wave_min_f32(bv);
+      if (fm < INFINITY) {
+        const int pl = uni(__builtin_ctzll(__ballot(bv == fm)));
+        pc = pl + LANES * uni(__builtin_amdgcn_readlane(bk, pl));
+        if constexpr (SharedT<NV>::kPair) {
+          const int vc = 3 * (pc / 6);
+          float bw = INFINITY;
+          int bk2 = 0;
+#pragma unroll
+          for (int k = 0; k < CPL; ++k) {
+            const float kk = cz[k] == vc ? INFINITY : keyf[k];
+            bk2 = kk < bw ? k : bk2;
+            bw = fminf(bw, kk);
+          }
+          const float fm2 = wave_min_f32(bw);
+          if (fm2 < INFINITY) {
+            const int ql = uni(__builtin_ctzll(__ballot(bw == fm2)));
+            pc2 = ql + LANES * uni(__builtin_amdgcn_readlane(bk2, ql));
+          }
+        }
+      }
+      if constexpr (kSplit) {
+        if (lane == 0)
+          __hip_atomic_store(&sm.choice, (((tag_it + 1) & 0xffff) << 16) | ((pc2 + 1) << 8) | (pc + 1),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      return;
+    }
+#endif
     double key[CPL];
 #pragma unroll
     for (int k = 0; k < CPL; ++k)
@@ -1116,16 +1158,22 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         }
         // rank-2 updates: row coefficients (al, be) = S^-1 (row's pair), then
         // M[r][c] -= al cz1[c] + be cz2[c]
-        if constexpr (kCurKey)
+        // q_c, the row metric, is read only by the choosing wave (wave 1 with the split choice)
+        auto qm_pair = [&]() {
+          if constexpr (kCurKey)
 #pragma unroll
-          for (int k = 0; k < CPL; ++k)
-            qm[k] = (float)((double)qm[k] - fma(i11 * zs[k], zs[k], fma(2.0 * i12 * zs[k], zs2[k], i22 * zs2[k] * zs2[k])));
+            for (int k = 0; k < CPL; ++k)
+              qm[k] = (float)((double)qm[k] - fma(i11 * zs[k], zs[k], fma(2.0 * i12 * zs[k], zs2[k], i22 * zs2[k] * zs2[k])));
+        };
         ++it;   // a pair step counts as the two additions it makes
         if constexpr (kEarly) {
           if (wave == 1) {   // the row values are final for this pass: choose now, before the FMAs
+            qm_pair();
             choose(it, epc, epc2);
             early = true;
           }
+        } else {
+          qm_pair();
         }
         SEC(17);
         double cz1[TW], cz2[TW], z41[4], z42[4];
@@ -1243,7 +1291,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       for (int k = VPL - 1; k >= 0; --k)
         if (~occ[k]) q = LANES * k + __builtin_ctzll(~occ[k]);
       const double is = rcp_nr(zsp);
-      if constexpr (kCurKey)
+      if constexpr (kCurKey && !kEarly)
 #pragma unroll
         for (int k = 0; k < CPL; ++k) qm[k] = (float)fma(-zs[k] * zs[k], is, (double)qm[k]);
       double zr4[4], rr4[4];
@@ -1269,6 +1317,9 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       p = -1;
       if constexpr (kEarly) {
         if (wave == 1) {   // the row values are final for this pass: choose before the FMAs
+          if constexpr (kCurKey)   // q_c is read only by the choosing wave
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) qm[k] = (float)fma(-zs[k] * zs[k], is, (double)qm[k]);
           choose(it, epc, epc2);
           early = true;
         }
@@ -1336,7 +1387,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     }
 #endif
     if (zrow >= 0) {
-      if constexpr (kCurKey) {
+      if (kCurKey && (!kSplit || wave == 1)) {   // q_c is read only by the choosing wave
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {   // q_c += (a_c . R_l)^2 / eta (sm.rl holds R_l until the next drop)
           const double ar = cdot(sm.rl, k);
