@@ -411,6 +411,11 @@ __device__ __forceinline__ double form_h_full(const FormY& fy, int N, int ja, in
 }
 
 // H[a][b] from the foot-steps' horizon steps (ja, jb) and input columns (ca, cb)
+// form_h with (Ta, m) of the step pair looked up (the same arithmetic, bitwise)
+__device__ __forceinline__ double form_h_tab(const FormY& fy, d2 tm, int ca, int cb) {
+  const d2 y = fy.Y[ca * NU + cb];
+  return 2.0 * fma(tm[1], y[1], tm[0] * y[0]);
+}
 __device__ __forceinline__ double form_h(const FormY& fy, int N, int ja, int ca, int jb, int cb) {
   const int mx = ja > jb ? ja : jb;
   const int d = ja > jb ? ja - jb : jb - ja;

@@ -48,6 +48,7 @@ template <int NV>
 struct FormArea {
   Form f;
   FormY fy;
+  d2 mt_tab[kMaxN * kMaxN];   // (Ta, m) of every foot-step step pair (ja, jb) for the diagonal-Q H build
 };
 template <int NV>
 struct alignas(16) SharedT {
@@ -83,6 +84,8 @@ struct alignas(16) SharedT {
   double wmax[Cfg<NV>::NW];
   int choice;   // class 64, MPCQP_SPLIT_CHOICE: wave 1's published {pass tag, p2 + 1, p + 1}
 };
+// the formulation scratch must not grow the H copy's union (class 64: 4 robots per CU)
+static_assert(sizeof(FormArea<64>) <= sizeof(double) * 64 * 64, "formulation scratch exceeds the H copy");
 
 constexpr int DPP_SHL1 = 0x101;   // row_shl:1 -- lane i reads lane i + 1 (same 16-lane row)
 constexpr int DPP_ROR8 = 0x128;   // row_ror:8 -- lane i <-> i ^ 8 inside 16 lanes
@@ -251,6 +254,17 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 
   // ------------------------------------------------ formulation (mpcqp_form.h)
   form_model<NT>(P, smf, smfy, sm.mt, N, tid);
+  if constexpr (!FULL) {
+    // the H build's integer block weights, once per step pair instead of once per entry
+    for (int e = tid; e < N * N; e += NT) {
+      const int ja = e / N, jb = e - ja * N;
+      const int mx = ja > jb ? ja : jb;
+      const int d = ja > jb ? ja - jb : jb - ja;
+      const int m = N - mx;
+      const int ta = (m * (4 * m * m - 1)) / 3 + 2 * d * m * m;   // exact integer
+      sm.fa.mt_tab[e] = d2{(double)ta, (double)m};
+    }
+  }
   fsync<NT>();
   if (tid < NV) sm.gv[tid] = tid < n ? form_g(P, smf, sm.mt, tid) : 0.0;
   STAMP(1);
@@ -279,7 +293,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       const int col = TW * tc + c;
       double hv;
       if constexpr (FULL) hv = form_h_full(smfy, N, ja, car, cj[c], cc[c]);
-      else hv = form_h(smfy, N, ja, car, cj[c], cc[c]) + (row == col ? r2 : 0.0);
+      else hv = form_h_tab(smfy, sm.fa.mt_tab[ja * N + cj[c]], car, cc[c]) + (row == col ? r2 : 0.0);
       h[c] = (row < n && col < n) ? hv : (row == col ? 1.0 : 0.0);
     }
   };
