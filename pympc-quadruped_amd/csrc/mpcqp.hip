@@ -82,6 +82,17 @@ static_assert(kMaxN == 20, "the dense classes' and the interior-point class's LD
 // row values, before its rank-1 / rank-2 FMAs, so wave 0 finds the choice published
 #define MPCQP_EARLY_CHOICE 1
 #endif
+#ifndef MPCQP_DROP_FUSE
+// class 64: a drop pass writes the next pass's z = P' a_p and r = R' a_p as rank-1
+// corrections of its own (the next pass retries the same row p), so that pass skips its
+// column combination and the barrier after it
+#define MPCQP_DROP_FUSE 0   // measured neutral (config 2 +-0 %, config 3 -0.5..+0.3 %), not bitwise: off
+#endif
+#ifndef MPCQP_SWEEP_PIPE
+// class 64's single-pivot H^-1 sweep software-pipelined: each pivot's update of the next
+// pivot's column at once, the other columns' FMAs deferred behind the next barrier
+#define MPCQP_SWEEP_PIPE 0   // bitwise identical, measured slower (config 2 -1.3 %, config 3 -1 %): off
+#endif
 #ifndef MPCQP_C64_SYMPAIR
 #define MPCQP_C64_SYMPAIR 1   // the one-wave sweep takes pivot pairs (one rank-2 pass each)
 #endif

@@ -609,6 +609,67 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       }
     });
   }
+  } else if constexpr (TW == 8 && MPCQP_SWEEP_PIPE) {
+  // The single-pivot pass below, software-pipelined: pivot K updates register column
+  // (K + 1) % 8 -- the next pivot's column, published at the top of the next step -- at
+  // once, and defers its other seven columns (and the -2 on its diagonal) into step
+  // K + 1, where those FMAs issue behind the barrier under the pivot-column loads and the
+  // reciprocal instead of ahead of the barrier.  Every entry still takes every pivot's
+  // FMA in pivot order: bitwise the same W.
+  double db[4] = {0.0, 0.0, 0.0, 0.0}, dz[TW], dfix = 0.0;
+#pragma unroll
+  for (int c = 0; c < TW; ++c) dz[c] = 0.0;
+#pragma unroll 1
+  for (int KT = 0; TW * KT < n; ++KT) {
+    static_for<TW>([&](auto KCc) {
+      constexpr int KC = decltype(KCc)::value;
+      constexpr int KP = (KC + TW - 1) % TW;   // the previous pivot's register column
+      constexpr int KN = (KC + 1) % TW;        // this pivot's eager column
+      const int K = TW * KT + KC;
+      const int KR = 2 * KT + (KC >> 2);
+      if (K < n) {
+        double* const zc = sm.zc[KC & 1];
+        if (tc == KT) {   // column KC took pivot K - 1 eagerly
+          d2* pz = reinterpret_cast<d2*>(zc + 4 * tr);
+          pz[0] = d2{W[0][KC], W[1][KC]};
+          pz[1] = d2{W[2][KC], W[3][KC]};
+        }
+        fsync<NT>();
+        const double dK = zc[K];   // first: the reciprocal waits for this load only
+        double zr[TW], zi[4];
+        ldt<TW>(zr, zc, tc);
+        ld4(zi, zc, tr);
+        // pivot K - 1's deferred columns (all but KC), then its diagonal fix-up
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int c = 0; c < TW; ++c)
+            if (c != KC) W[r][c] = fma(db[r], dz[c], W[r][c]);
+        W[KP & 3][KP] += dfix;
+        const double inv = rcp_nr(dK);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) db[r] = -zi[r] * inv;
+        if (tr == KR) db[KC & 3] = inv - 1.0;
+        if (tc == KT) zr[KC] = dK - 1.0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) W[r][KN] = fma(db[r], zr[KN], W[r][KN]);
+#pragma unroll
+        for (int c = 0; c < TW; ++c) dz[c] = zr[c];
+        dfix = (tc == KT && tr == KR) ? -2.0 : 0.0;
+      }
+    });
+  }
+  {   // the last pivot's deferred columns (its eager column is n % 8)
+    const int kn = n & (TW - 1), kp = (n - 1) & (TW - 1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < TW; ++c)
+        if (c != kn) W[r][c] = fma(db[r], dz[c], W[r][c]);
+#pragma unroll
+    for (int c = 0; c < TW; ++c)
+      if (c == kp) W[c & 3][c] += dfix;
+  }
   } else {
   // pivot K = 8 KT + KC: W_ij -= z_i z_j / d, W_iK = z_i / d, W_KK = -1/d (ends at
   // -H^-1; padding rows/columns >= n never change).  One generic rank-1 pass (the
@@ -900,6 +961,9 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   };
   bool early = false;   // kEarly: wave 1 already holds (and has published) the next choice
   int epc = -1, epc2 = -1;
+  // kDropFuse: the previous pass dropped a slot and left this pass's z / r in its buffers
+  constexpr bool kDropFuse = NV == 64 && VPL == 1 && C::NW == 2 && MPCQP_DROP_FUSE;
+  bool fused = false;
   SEC(0);
   while (true) {
     // pair candidate p2 (another foot-step's most violated row), set on a fresh choice
@@ -1052,6 +1116,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     double* const vr = sm.vr[buf];
     double* const vz2 = sm.zc[buf];
     double* const vr2 = sm.vr2[buf];
+    if (!(kDropFuse && fused)) {   // after a drop z and r are already in vz / vr (p2 < 0)
     combo_store(c0, tcA, a0, a1, a2, vz, vr);
     if (p2 >= 0) combo_store(c02, tcA2, b0, b1, b2, vz2, vr2);
 #if MPCQP_DUP == 1   // diagnostic: the combos twice (same values), to price them on the critical path
@@ -1067,6 +1132,8 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #if MPCQP_DUP == 3   // diagnostic: one more workgroup barrier per pass
     fsync<NT>();
 #endif
+    }
+    fused = false;
     SEC(2);
     // constraint-row steps zs = A z, slot directions r, variable steps
     double zs[CPL];
@@ -1373,6 +1440,15 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       fsync<NT>();
       const double ie = rcp_nr(sm.yv[l]);
       iedrop = ie;
+      if constexpr (kDropFuse) {
+        // the next pass retries p: z' = P' a_p = z + (r_l / eta) R_l^T and r' = R' a_p =
+        // r - (r_l / eta) y, r'_l = 0 (r_l = R_l . a_p), into its buffers (wave 0 z', wave 1
+        // r'; visible after this pass's closing barrier), instead of its column combinations
+        const double cf = vr[l] * ie;
+        if (wave == 0) sm.vz[buf ^ 1][lane] = fma(cf, sm.rl[lane], vz[lane]);
+        else sm.vr[buf ^ 1][lane] = lane == l ? 0.0 : fma(-cf, sm.yv[lane], vr[lane]);
+        fused = true;
+      }
       double rl4[4], yv4[4];
       ld4(rl4, sm.rl, tr);
       ld4(yv4, sm.yv, tr);
