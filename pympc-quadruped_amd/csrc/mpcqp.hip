@@ -93,6 +93,11 @@ static_assert(kMaxN == 20, "the dense classes' and the interior-point class's LD
 // pivot's column at once, the other columns' FMAs deferred behind the next barrier
 #define MPCQP_SWEEP_PIPE 0   // bitwise identical, measured slower (config 2 -1.3 %, config 3 -1 %): off
 #endif
+#ifndef MPCQP_SWEEP_PIPE2
+// classes 96 / 128: the pivot-pair H^-1 sweep software-pipelined (the next pair's columns
+// at once, the other columns' FMAs deferred behind the next barrier)
+#define MPCQP_SWEEP_PIPE2 0   // bitwise identical, measured slower (config 4 -1.8 %, config 5 -2.5 %): off
+#endif
 #ifndef MPCQP_C64_SYMPAIR
 #define MPCQP_C64_SYMPAIR 1   // the one-wave sweep takes pivot pairs (one rank-2 pass each)
 #endif

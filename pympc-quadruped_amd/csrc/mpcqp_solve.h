@@ -523,6 +523,128 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         sm.ht[(TW * r + c) * NT + tid] = W[r][c];
         W[r][c] = Ws[r][c];
       }
+  } else if constexpr (NV >= 96 && MPCQP_SWEEP_PIPE2) {
+  // The pivot-pair pass below, software-pipelined (one robot per CU: the sweep is a
+  // latency chain here, not issue-bound as class 64's four robots are): pair {K, K + 1}
+  // updates the next pair's two register columns at once and defers its other columns
+  // (and the -2 on its diagonal) behind the next pair's barrier, where they issue under
+  // the pivot-column loads and the 2 x 2 inverse.  Each entry takes every pair's FMAs in
+  // pair order: bitwise the same W.
+  double dc0[4], dc1[4], dr0[TW], dr1[TW], dfix = 0.0;
+  int dkrr = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    dc0[r] = 0.0;
+    dc1[r] = 0.0;
+  }
+#pragma unroll
+  for (int c = 0; c < TW; ++c) {
+    dr0[c] = 0.0;
+    dr1[c] = 0.0;
+  }
+  // the -2 on a pair's diagonal (columns kc, kc + 1, rows krr, krr + 1 of the lane holding it)
+  auto pair_fix = [&](auto kcc, int krr, double fx) {
+    constexpr int kc = decltype(kcc)::value;
+    if constexpr (TW == 8) {
+      W[kc & 3][kc] -= fx;
+      W[(kc & 3) + 1][kc + 1] -= fx;
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; r += 2) {
+        W[r][kc] -= r == krr ? fx : 0.0;
+        W[r + 1][kc + 1] -= r == krr ? fx : 0.0;
+      }
+    }
+  };
+#pragma unroll 1
+  for (int KT = 0; TW * KT < n; ++KT) {
+    static_for<TW / 2>([&](auto KPc) {
+      constexpr int KC = 2 * decltype(KPc)::value;
+      constexpr int KP = (KC + TW - 2) % TW;   // the previous pair's first register column
+      constexpr int KN = (KC + 2) % TW;        // this pair's eager columns KN, KN + 1
+      const int K = TW * KT + KC;
+      const int KR = TW == 8 ? 2 * KT + (KC >> 2) : K >> 2;
+      const int KRR = TW == 8 ? (KC & 3) : (K & 3);   // 0 or 2
+      if (K < n) {
+        double* const z0 = sm.zc[0] + ((K >> 1) & 1) * (2 * C::VEC);
+        double* const z1 = z0 + C::VEC;
+        if (tc == KT) {   // columns KC, KC + 1 took the previous pair eagerly
+          d2* q0 = reinterpret_cast<d2*>(z0 + 4 * tr);
+          q0[0] = d2{W[0][KC], W[1][KC]};
+          q0[1] = d2{W[2][KC], W[3][KC]};
+          d2* q1 = reinterpret_cast<d2*>(z1 + 4 * tr);
+          q1[0] = d2{W[0][KC + 1], W[1][KC + 1]};
+          q1[1] = d2{W[2][KC + 1], W[3][KC + 1]};
+        }
+        fsync<NT>();
+        const double d00 = z0[K], d01 = z0[K + 1], d11 = z1[K + 1];   // first: the inverse waits for these
+        double zr0[TW], zr1[TW], zi0[4], zi1[4];
+        ldt<TW>(zr0, z0, tc);
+        ldt<TW>(zr1, z1, tc);
+        ld4(zi0, z0, tr);
+        ld4(zi1, z1, tr);
+        // the previous pair's deferred columns (all but KC, KC + 1), then its diagonal
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int c = 0; c < TW; ++c)
+            if (c != KC && c != KC + 1) W[r][c] = fma(dc1[r], dr1[c], fma(dc0[r], dr0[c], W[r][c]));
+        pair_fix(std::integral_constant<int, KP>{}, dkrr, dfix);
+        const double idet = rcp_nr(fma(d00, d11, -d01 * d01));
+        const double e00 = d11 * idet, e01 = -d01 * idet, e11 = d00 * idet;   // D^-1
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          dc0[r] = -fma(zi0[r], e00, zi1[r] * e01);
+          dc1[r] = -fma(zi0[r], e01, zi1[r] * e11);
+        }
+        if constexpr (TW == 8) {
+          if (tr == KR) {
+            dc0[KRR] = e00 - 1.0;
+            dc1[KRR] = e01;
+            dc0[KRR + 1] = e01;
+            dc1[KRR + 1] = e11 - 1.0;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; r += 2) {
+            const bool at = tr == KR && r == KRR;
+            dc0[r] = at ? e00 - 1.0 : dc0[r];
+            dc1[r] = at ? e01 : dc1[r];
+            dc0[r + 1] = at ? e01 : dc0[r + 1];
+            dc1[r + 1] = at ? e11 - 1.0 : dc1[r + 1];
+          }
+        }
+        if (tc == KT) {   // the pair's columns enter with D - I
+          zr0[KC] -= 1.0;
+          zr1[KC + 1] -= 1.0;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int c = KN; c < KN + 2; ++c) W[r][c] = fma(dc1[r], zr1[c], fma(dc0[r], zr0[c], W[r][c]));
+#pragma unroll
+        for (int c = 0; c < TW; ++c) {
+          dr0[c] = zr0[c];
+          dr1[c] = zr1[c];
+        }
+        dfix = (tc == KT && tr == KR) ? 2.0 : 0.0;
+        dkrr = KRR;
+      }
+    });
+  }
+  {   // the last pair's deferred columns and diagonal (its eager columns: kn, kn + 1)
+    const int kl = ((n - 1) >> 1) << 1;   // the last pair's first pivot
+    const int kc = kl % TW, kn = (kc + 2) % TW;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < TW; ++c)
+        if (c != kn && c != kn + 1) W[r][c] = fma(dc1[r], dr1[c], fma(dc0[r], dr0[c], W[r][c]));
+    static_for<TW / 2>([&](auto KPc) {
+      constexpr int KC = 2 * decltype(KPc)::value;
+      if (kc == KC) pair_fix(std::integral_constant<int, KC>{}, dkrr, dfix);
+    });
+  }
   } else if constexpr (NV >= 96) {
   // Classes 96 / 128 (one robot per CU, latency-bound; 6- / 8-wave barriers):
   // pivot PAIRS {K, K + 1} (K even: one tile column, one 4-row group; K + 1 = n is
