@@ -88,6 +88,27 @@ def cpu_baseline(bt, N, budget_s, threads=1):
     return done / dt, done, dt, tf / done, ts / done
 
 
+def cpu_baseline_line(bt, N, seconds, world):
+    """The `cpu_baseline` object: the compiled port timed on this host's cores (rank 0 only,
+    after the measured region -- with N > 1 the other ranks are idle by then), 16 threads
+    (the box's CPU share per GPU) and 1 thread, half of `seconds` each."""
+    procs = _host_cores()
+    v1, done1, dt1, f1, s1 = cpu_baseline(bt, N, seconds / 2, threads=1)
+    vm, donem, dtm, fm, sm_ = cpu_baseline(bt, N, seconds / 2, threads=procs)
+    cpu = {"value": vm, "unit": "QP/s", "cores": procs, "kind": "port",
+           "sample": f"{donem} robot solves (the config's first synthetic batch, cycled) in {dtm:.1f}s, "
+                     f"OpenMP {procs} threads ({_cpu_model()}): compiled restatement of the reference's "
+                     "formulation (float32 model, dense condensing, mpc.py:173-260) + float64 "
+                     "Goldfarb-Idnani QP (oracle/cpu_mpc.cpp, g++ -O3)",
+           "formulation_us_per_robot": fm * 1e6, "solve_us_per_robot": sm_ * 1e6,
+           "single_core": {"value": v1, "cores": 1, "formulation_us": f1 * 1e6, "solve_us": s1 * 1e6,
+                           "sample": f"{done1} robots in {dt1:.1f}s, 1 thread"}}
+    if world > 1:
+        cpu["note"] = (f"timed on rank 0's host after the {world}-rank measured region: one host's "
+                       f"{procs} threads, not {world} hosts' -- the same baseline as the N = 1 line")
+    return cpu
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as fh:
@@ -225,14 +246,20 @@ def rehearse_cpu(args, world, rank, dist):
     if world > 1:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     if rank == 0:
+        el = float(tmax.item())
+        cpu = None if args.no_cpu else cpu_baseline_line(h, N, args.cpu_seconds, world)
         print(json.dumps({"metric": "QP solves/sec (whole node), horizon=10 GRF QP, at 1/2/4/8 MI355X",
-                          "value": world * Bpg * args.steps / float(tmax.item()), "unit": "QP/s",
-                          "n_gpus": world, "steps": args.steps, "warmup": 0, "rehearsal": True,
+                          "value": world * Bpg * args.steps / el, "unit": "QP/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": 0,
+                          "ms_per_step": el / max(args.steps, 1) * 1e3, "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+                          "data": "synthetic (seeded SURVEY §8(d) states; seed = base + rank)",
+                          "roofline": None, "cpu_baseline": cpu, "rehearsal": True,
                           "note": "gloo rehearsal on CPU tensors: stand-in solve (zero fill), not a measurement",
                           "gathered_rows": rows, "gather_ok": gather_ok, "x0_rows": int(x0.shape[0]),
                           "per_rank_batch": per_rank, "horizon": N,
                           "config": {"workload": f"{args.config}: {total} robots over {world} ranks",
-                                     "global_batch": total,
+                                     "batch_per_gpu": Bpg, "horizon": N, "global_batch": total,
                                      "parallelism": f"robot-sharded x{world} + gloo all-gather of u0"}}))
     if world > 1:
         dist.destroy_process_group()
@@ -568,19 +595,7 @@ def main():
         be = dist.get_backend()
         gather_label = " + " + ("RCCL" if be == "nccl" else be) + " all-gather of u0"
     if rank == 0:
-        cpu = None
-        if world == 1 and not args.no_cpu:
-            procs = _host_cores()
-            v1, done1, dt1, f1, s1 = cpu_baseline(host[0], N, args.cpu_seconds / 2, threads=1)
-            vm, donem, dtm, fm, sm_ = cpu_baseline(host[0], N, args.cpu_seconds / 2, threads=procs)
-            cpu = {"value": vm, "unit": "QP/s", "cores": procs, "kind": "port",
-                   "sample": f"{donem} robot solves (the config's first synthetic batch, cycled) in {dtm:.1f}s, "
-                             f"OpenMP {procs} threads ({_cpu_model()}): compiled restatement of the reference's "
-                             "formulation (float32 model, dense condensing, mpc.py:173-260) + float64 "
-                             "Goldfarb-Idnani QP (oracle/cpu_mpc.cpp, g++ -O3)",
-                   "formulation_us_per_robot": fm * 1e6, "solve_us_per_robot": sm_ * 1e6,
-                   "single_core": {"value": v1, "cores": 1, "formulation_us": f1 * 1e6, "solve_us": s1 * 1e6,
-                                   "sample": f"{done1} robots in {dt1:.1f}s, 1 thread"}}
+        cpu = None if args.no_cpu else cpu_baseline_line(host[0], N, args.cpu_seconds, world)
         line = {
             "metric": "QP solves/sec (whole node), horizon=10 GRF QP, at 1/2/4/8 MI355X",
             "value": qps,

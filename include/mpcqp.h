@@ -21,6 +21,11 @@
  * No exception crosses the ABI: every entry point returns MPCQP_OK (0) or a
  * negative error code; mpcqp_last_error() describes the last failure.
  * Per-robot solver outcome is reported in status[] (MPCQP_STATUS_*).
+ * A context keeps per-stream device queues for up to 8 streams; a solve on a 9th
+ * distinct stream takes over the least recently used stream's queues after a whole-
+ * device synchronisation (hipDeviceSynchronize: it waits for every stream, and fails
+ * while a stream is being captured into a graph).  Round-robin over at most 8 streams
+ * per context to stay asynchronous.
  *
  * Layouts (float32, row-major, robot-major):
  *   x0      [B][13]   [roll, pitch, yaw, px, py, pz, wx, wy, wz, vx, vy, vz, -g]
@@ -104,9 +109,13 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
 
 /* Full state / input weights (mpc.py:49-52 builds kron(I_N, Q), kron(I_N, R) from any
  * LinearMpcConfig.Q / R): Q [13][13] and R [12][12] row-major HOST arrays, symmetric and
- * finite (else MPCQP_ERR_ARG); NULL keeps the current diagonal of that matrix.  Diagonal
- * matrices select the diagonal fast path (equivalent to setting q_diag / r_diag).  The
- * weights are copied before the call returns; solves issued before it are unaffected.
+ * finite (else MPCQP_ERR_ARG); NULL keeps the current matrix (as last set, off-diagonal
+ * entries included).  Diagonal matrices select the diagonal fast path (equivalent to
+ * setting q_diag / r_diag).  The weights are copied before the call returns; solves issued
+ * before it are unaffected.  A failed call (error code) leaves the previous weights in
+ * force.  Cost: when full weights were in force, the call synchronises the whole device
+ * (hipDeviceSynchronize) before releasing their buffer -- do not call it while a stream
+ * of this device is being captured into a graph.
  * The interior-point class (robots with more than 128 stance variables) supports a full
  * Q and an R without cross-leg couplings (R[i][j] = 0 for legs i / 3 != j / 3); a robot of
  * that class under weights it does not support reports MPCQP_STATUS_UNSUPPORTED. */

@@ -43,9 +43,6 @@ constexpr int NU = 12;      // input dimension (mpc.py:28)
 constexpr int LANES = 64;
 constexpr int kMaxN = MPCQP_MAX_HORIZON;   // LDS scratch is sized for N <= 20 (include/mpcqp.h)
 static_assert(kMaxN == 20, "the dense classes' and the interior-point class's LDS layouts are sized for N <= 20");
-#ifndef MPCQP_C64_TW
-#define MPCQP_C64_TW 8   // class-64 register tile width (8: 2 waves per robot; 4: 4 waves, slower)
-#endif
 #ifndef MPCQP_SPLIT_CHOICE
 #define MPCQP_SPLIT_CHOICE 1   // class 64: wave 1 chooses the next rows, wave 0 reads them; 0: both choose
 #endif
@@ -54,14 +51,6 @@ static_assert(kMaxN == 20, "the dense classes' and the interior-point class's LD
 #endif
 #ifndef MPCQP_CURKEY_MAX_NV
 #define MPCQP_CURKEY_MAX_NV 64   // row choice in the current projected metric up to this class
-#endif
-#ifndef MPCQP_SWEEP_MFMA
-#define MPCQP_SWEEP_MFMA 0   // 1: class-64 H^-1 sweep blocked by 4 pivots on the f64 MFMA (parity-exact, slower: DESIGN 4.5)
-#endif
-#ifndef MPCQP_C64_SYMSWEEP
-// 1: class 64 takes n <= 60 and inverts H on ONE wave holding its 64 lower 4 x 8 tiles
-// (no barrier per pivot, half the VALU of the two-wave sweep); n = 61..64 go to class 96
-#define MPCQP_C64_SYMSWEEP 0   // measured slower: off
 #endif
 #ifndef MPCQP_ASM_COMBO
 // class 64's z / r column combination as one computed jump (mpcqp_combo_asm.h) instead of
@@ -74,41 +63,17 @@ static_assert(kMaxN == 20, "the dense classes' and the interior-point class's LD
 #ifndef MPCQP_F32_KEY
 #define MPCQP_F32_KEY 1   // row keys in f32 throughout (not bitwise identical to f64 keys: near-ties may resolve differently)
 #endif
-#ifndef MPCQP_DUP
-#define MPCQP_DUP 0   // diagnostic builds only: duplicate one loop component (tools/gpu_ab.sh pricing)
-#endif
 #ifndef MPCQP_EARLY_CHOICE
 // class 64 split choice: wave 1 chooses the next rows as soon as the pass has updated the
 // row values, before its rank-1 / rank-2 FMAs, so wave 0 finds the choice published
 #define MPCQP_EARLY_CHOICE 1
-#endif
-#ifndef MPCQP_DROP_FUSE
-// class 64: a drop pass writes the next pass's z = P' a_p and r = R' a_p as rank-1
-// corrections of its own (the next pass retries the same row p), so that pass skips its
-// column combination and the barrier after it
-#define MPCQP_DROP_FUSE 0   // measured neutral (config 2 +-0 %, config 3 -0.5..+0.3 %), not bitwise: off
-#endif
-#ifndef MPCQP_SWEEP_PIPE
-// class 64's single-pivot H^-1 sweep software-pipelined: each pivot's update of the next
-// pivot's column at once, the other columns' FMAs deferred behind the next barrier
-#define MPCQP_SWEEP_PIPE 0   // bitwise identical, measured slower (config 2 -1.3 %, config 3 -1 %): off
-#endif
-#ifndef MPCQP_SWEEP_PIPE2
-// classes 96 / 128: the pivot-pair H^-1 sweep software-pipelined (the next pair's columns
-// at once, the other columns' FMAs deferred behind the next barrier)
-#define MPCQP_SWEEP_PIPE2 0   // bitwise identical, measured slower (config 4 -1.8 %, config 5 -2.5 %): off
-#endif
-#ifndef MPCQP_C64_SYMPAIR
-#define MPCQP_C64_SYMPAIR 1   // the one-wave sweep takes pivot pairs (one rank-2 pass each)
-#endif
-#ifndef MPCQP_C64_WPE
-#define MPCQP_C64_WPE (MPCQP_C64_TW == 4 ? 4 : 2)   // class-64 waves per SIMD (VGPR budget)
 #endif
 // staged inputs (floats)
 constexpr int IN_X0 = 0, IN_FEET = 13, IN_ROBOT = 25, IN_CONTACT = 44, IN_XREF = 44 + 4 * kMaxN;
 constexpr int IN_END = IN_XREF + NX * kMaxN;
 
 typedef double d2 __attribute__((ext_vector_type(2)));
+typedef double d4 __attribute__((ext_vector_type(4)));   // v_mfma_f64_16x16x4 accumulators (mpcqp_ipm.h)
 
 struct KParams {
   int N;
@@ -358,7 +323,6 @@ __device__ __forceinline__ int wave_argmin_f32(double v, double& vmin_out) {
 }
 
 #include "mpcqp_form.h"
-#include "mpcqp_sweep_mfma.h"
 #include "mpcqp_combo_asm.h"
 #include "mpcqp_solve.h"
 #include "mpcqp_ipm.h"
@@ -376,13 +340,13 @@ __device__ __forceinline__ int xcd_robot(int bid, int B) {
 }
 
 // class 64's capacity (stance variables): 60 with the one-wave symmetric sweep
-constexpr int kCap64 = MPCQP_C64_SYMSWEEP ? 60 : 64;
+constexpr int kCap64 = 64;
 
 // Class NV = 64: one 2-wave workgroup per robot of the batch.  Robots with more
 // than 64 stance variables are appended to `queue` (when given) for class 96, those
 // with more than 96 to `queue_big` (when given) for class 128.
 template <bool FULL>
-__global__ __launch_bounds__(Cfg<64>::NT) __attribute__((amdgpu_waves_per_eu(MPCQP_C64_WPE, Cfg<64>::NW))) void mpcqp_kernel_64(
+__global__ __launch_bounds__(Cfg<64>::NT) __attribute__((amdgpu_waves_per_eu(2, Cfg<64>::NW))) void mpcqp_kernel_64(
     KParams P, int B, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
@@ -521,6 +485,8 @@ struct mpcqp_ctx {
   std::vector<QueueSet> queues;
   unsigned long long use_clock;
   double* wdev;       // full Q (13 x 13) then R (12 x 12) on the device (mpcqp_set_weights); nullptr: diagonal
+  double q_full[13 * 13];   // the current weights as whole matrices (host copies: a NULL argument
+  double r_full[12 * 12];   // of mpcqp_set_weights keeps that matrix, off-diagonal entries included)
   double dt_control;  // planner constants (mpcqp_set_planner)
   double gravity;
   double max_pos_error;
@@ -650,6 +616,8 @@ int mpcqp_create(const mpcqp_params* p, int32_t device, mpcqp_ctx** out) {
   ctx->ncu = 0;
   ctx->use_clock = 0;
   ctx->wdev = nullptr;
+  for (int i = 0; i < 13 * 13; ++i) ctx->q_full[i] = (i % 14 == 0) ? p->q_diag[i / 14] : 0.0;
+  for (int i = 0; i < 12 * 12; ++i) ctx->r_full[i] = (i % 13 == 0) ? p->r_diag[i / 13] : 0.0;
   ctx->dt_control = 0.001;    // linear_mpc_configs.py:6
   ctx->gravity = 9.81;        // linear_mpc_configs.py:13
   ctx->max_pos_error = 0.1;   // mpc.py:121
@@ -776,10 +744,8 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
 int mpcqp_set_weights(mpcqp_ctx* ctx, const double* Q, const double* R) {
   if (!ctx) return MPCQP_ERR_ARG;
   double q[NX * NX], r[NU * NU];
-  for (int i = 0; i < NX * NX; ++i) q[i] = (i % (NX + 1) == 0) ? ctx->params.q_diag[i / (NX + 1)] : 0.0;
-  for (int i = 0; i < NU * NU; ++i) r[i] = (i % (NU + 1) == 0) ? ctx->params.r_diag[i / (NU + 1)] : 0.0;
-  if (Q) memcpy(q, Q, sizeof(q));
-  if (R) memcpy(r, R, sizeof(r));
+  memcpy(q, Q ? Q : ctx->q_full, sizeof(q));   // NULL keeps the current matrix
+  memcpy(r, R ? R : ctx->r_full, sizeof(r));
   // symmetric and finite (the reference's kron(I_N, Q) enters H = 2 Su^T Qbar Su; an
   // asymmetric Q would make H asymmetric, which no QP solver of the reference accepts)
   double qmax = 0.0, rmax = 0.0;
@@ -804,30 +770,36 @@ int mpcqp_set_weights(mpcqp_ctx* ctx, const double* Q, const double* R) {
       if (fabs(r[i * NU + j] - r[j * NU + i]) > 1e-12 * rmax) return set_err(ctx, MPCQP_ERR_ARG, "weights: R not symmetric");
       if (i != j && r[i * NU + j] != 0.0) diag = false;
     }
-  for (int i = 0; i < NX; ++i) ctx->params.q_diag[i] = q[i * (NX + 1)];
-  for (int i = 0; i < NU; ++i) ctx->params.r_diag[i] = r[i * (NU + 1)];
   DeviceScope dev(ctx->device);
   if (!dev.ok) return set_err(ctx, MPCQP_ERR_HIP, "hipSetDevice failed");
-  if (diag) {   // the diagonal fast path (the weights live in the kernel arguments)
-    if (ctx->wdev) {
-      if (hipDeviceSynchronize() != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, "weights: device sync failed");
-      (void)hipFree(ctx->wdev);
-      ctx->wdev = nullptr;
+  // Device work first, into a fresh buffer; the context changes only once it all succeeded
+  // (a failed allocation or upload leaves the previous weights in force).
+  double* nb = nullptr;
+  if (!diag) {
+    if (hipMalloc(&nb, sizeof(double) * (NX * NX + NU * NU)) != hipSuccess)
+      return set_err(ctx, MPCQP_ERR_ALLOC, "weights: allocation failed");
+    double host[NX * NX + NU * NU];
+    memcpy(host, q, sizeof(q));
+    memcpy(host + NX * NX, r, sizeof(r));
+    if (hipMemcpy(nb, host, sizeof(host), hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipFree(nb);
+      return set_err(ctx, MPCQP_ERR_HIP, "weights: upload failed");
     }
-    return MPCQP_OK;
   }
-  // launches on any stream (non-blocking ones included) may still read the previous weights
-  if (ctx->wdev && hipDeviceSynchronize() != hipSuccess)
-    return set_err(ctx, MPCQP_ERR_HIP, "weights: device sync failed");
-  if (!ctx->wdev && hipMalloc(&ctx->wdev, sizeof(double) * (NX * NX + NU * NU)) != hipSuccess) {
-    ctx->wdev = nullptr;
-    return set_err(ctx, MPCQP_ERR_ALLOC, "weights: allocation failed");
+  // launches on any stream (non-blocking ones included) may still read the previous
+  // buffer: it is released after a device synchronisation (the cost of a weight change)
+  if (ctx->wdev) {
+    if (hipDeviceSynchronize() != hipSuccess) {
+      if (nb) (void)hipFree(nb);
+      return set_err(ctx, MPCQP_ERR_HIP, "weights: device sync failed");
+    }
+    (void)hipFree(ctx->wdev);
   }
-  double host[NX * NX + NU * NU];
-  memcpy(host, q, sizeof(q));
-  memcpy(host + NX * NX, r, sizeof(r));
-  if (hipMemcpy(ctx->wdev, host, sizeof(host), hipMemcpyHostToDevice) != hipSuccess)
-    return set_err(ctx, MPCQP_ERR_HIP, "weights: upload failed");
+  ctx->wdev = nb;   // nullptr: the diagonal fast path (the weights live in the kernel arguments)
+  memcpy(ctx->q_full, q, sizeof(q));
+  memcpy(ctx->r_full, r, sizeof(r));
+  for (int i = 0; i < NX; ++i) ctx->params.q_diag[i] = q[i * (NX + 1)];
+  for (int i = 0; i < NU; ++i) ctx->params.r_diag[i] = r[i * (NU + 1)];
   return MPCQP_OK;
 }
 

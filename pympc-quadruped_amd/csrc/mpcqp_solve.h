@@ -27,8 +27,8 @@
 
 template <int NV>
 struct Cfg {
-  // tile width: 4 x TW register tiles (class 64: TW = 4 spreads a robot over 4 waves)
-  static constexpr int TW = NV == 96 ? 6 : (NV == 64 ? MPCQP_C64_TW : 8);
+  // tile width: 4 x TW register tiles
+  static constexpr int TW = NV == 96 ? 6 : 8;
   static constexpr int NW = NV * NV / (4 * TW * LANES);   // waves per robot
   static constexpr int NT = NW * LANES;
   static constexpr int TCN = NV / TW;         // tile columns (lanes per tile row)
@@ -95,14 +95,6 @@ __device__ __forceinline__ double dpp_shl1(double v) {
   const int lo = __builtin_amdgcn_update_dpp(0, (int)bits, DPP_SHL1, 0xF, 0xF, true);
   const int hi = __builtin_amdgcn_update_dpp(0, (int)(bits >> 32), DPP_SHL1, 0xF, 0xF, true);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-// Class 64 with the one-wave sweep: a symmetric 60 x 60 matrix (64 x 64 with padding)
-// held as its 64 lower 4 x 8 tiles (tile rows br < 15, tile columns bc <= br / 2, in
-// row-major order): tile L = lt_idx(br, bc), element 8 r + c at base[(8 r + c) * 64 + L]
-__device__ __forceinline__ int lt_idx(int br, int bc) {
-  const int m = br >> 1;
-  return ((br & 1) ? (m + 1) * (m + 1) : m * (m + 1)) + bc;
 }
 
 // Sum 4 row partials over the TCN lanes of a tile row.  Lane keeps row
@@ -235,10 +227,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   fsync<NT>();
   const int S = uni(sm.mt.S);
   const int n = 3 * S, m = 6 * S;
-  // class 64 with the one-wave symmetric sweep holds n <= 60 (15 tile rows: 64 lower tiles)
-  constexpr bool kSym = NV == 64 && MPCQP_C64_SYMSWEEP && TW == 8 && C::NW == 2;
-  constexpr int kCap = kSym ? 60 : NV;
-  if (n > kCap) {
+  if (n > NV) {
     // the next capacity class takes it: `queue`, `queue_big` (when given) for a robot
     // beyond class 96 as well, `queue_ipm` (when given) for one beyond class 128
     int* qn = queue;
@@ -304,348 +293,15 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
     for (int r = 0; r < 4; ++r) hrow(r, cj, cc, W[r]);   // unrolled: rows land in their registers
   }
-  constexpr bool kMfmaSweep = NV == 64 && MPCQP_SWEEP_MFMA;
   fsync<NT>();   // every lane is done reading the formulation scratch H overwrites
-  if constexpr (kSym) {
-    // H's 64 lower tiles (tile rows < 15, tc <= tr / 2) into the first half of ht; the
-    // second half stages the sweep's result
-    // (unconditional stores: the other lanes write into the still-dead staging half, so the
-    // H build is not sunk into a branch -- in the full-weight kernel that spilled)
-    const int L = (tr < 15 && tc <= (tr >> 1)) ? lt_idx(tr, tc) : 2048 + lane;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+  for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int c = 0; c < TW; ++c) sm.ht[(TW * r + c) * LANES + L] = W[r][c];
-  } else if constexpr (!kMfmaSweep) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int c = 0; c < TW; ++c) sm.ht[(TW * r + c) * NT + tid] = W[r][c];
-  }
+    for (int c = 0; c < TW; ++c) sm.ht[(TW * r + c) * NT + tid] = W[r][c];
   STAMP(2);
 
   // ------------------------------------------------ W = H^-1 (symmetric sweep)
-  if constexpr (kSym) {
-    // Class 64, n <= 60: wave 0 sweeps the 64 lower 4 x 8 tiles of H, one per lane (tile
-    // L = lt_idx(br, bc)), with the full-tile pass's arithmetic: the pivot column K is
-    // assembled in LDS from column K of the tiles in tile column K / 8 (rows >= 8 (K / 8))
-    // and row K of the tiles in tile row K / 4 (columns < 8 (K / 8) + 8); the entries of
-    // the diagonal tiles above the diagonal ride along as the symmetric copies.  One wave:
-    // no workgroup barrier per pivot, and the four robots of a CU sweep on their wave 0,
-    // one per SIMD, instead of eight waves sharing the four SIMDs.  Wave 1 waits.
-    fsync<NT>();   // H's lower tiles are in LDS
-    if (wave == 0) {
-      int br = 0;
-#pragma unroll
-      for (int bb = 1; bb < 15; ++bb) br = lt_idx(bb, 0) <= lane ? bb : br;
-      const int bc = lane - lt_idx(br, 0);
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < TW; ++c) W[r][c] = sm.ht[(TW * r + c) * LANES + lane];
-      double* const zc = sm.zc[0];
-      double* const zc1 = sm.zc[1];
-      if (lane < 4) {   // rows 60..63: no tile holds them (padding)
-        zc[60 + lane] = 0.0;
-        zc1[60 + lane] = 0.0;
-      }
-#if MPCQP_C64_SYMPAIR
-      // pivot pairs {K, K + 1} (K even; K + 1 = n is the decoupled identity padding when n
-      // is odd), one rank-2 pass each as in classes 96 / 128: half the pivot chains
-#pragma unroll 1
-      for (int KT = 0; TW * KT < n; ++KT) {
-        static_for<TW / 2>([&](auto KPc) {
-          constexpr int KC = 2 * decltype(KPc)::value;
-          constexpr int KRR = KC & 3;   // 0 or 2
-          const int K = TW * KT + KC;
-          const int KR = 2 * KT + (KC >> 2);
-          if (K < n) {
-            if (br == KR) {   // rows K, K + 1: columns 8 bc .. 8 bc + 7
-              double r0[TW], r1[TW];
-#pragma unroll
-              for (int c = 0; c < TW; ++c) {
-                r0[c] = W[KRR][c];
-                r1[c] = W[KRR + 1][c];
-              }
-              stt<TW>(zc, bc, r0);
-              stt<TW>(zc1, bc, r1);
-            }
-            if (bc == KT) {   // columns K, K + 1: rows 4 br .. 4 br + 3 (written last)
-              d2* p0 = reinterpret_cast<d2*>(zc + 4 * br);
-              d2* p1 = reinterpret_cast<d2*>(zc1 + 4 * br);
-              p0[0] = d2{W[0][KC], W[1][KC]};
-              p0[1] = d2{W[2][KC], W[3][KC]};
-              p1[0] = d2{W[0][KC + 1], W[1][KC + 1]};
-              p1[1] = d2{W[2][KC + 1], W[3][KC + 1]};
-            }
-            fsync<LANES>();
-            double zr0[TW], zr1[TW], zi0[4], zi1[4];
-            ldt<TW>(zr0, zc, bc);
-            ldt<TW>(zr1, zc1, bc);
-            ld4(zi0, zc, br);
-            ld4(zi1, zc1, br);
-            const double d00 = zc[K], d01 = zc[K + 1], d11 = zc1[K + 1];
-            const double idet = rcp_nr(fma(d00, d11, -d01 * d01));
-            const double e00 = d11 * idet, e01 = -d01 * idet, e11 = d00 * idet;   // D^-1
-            double c0[4], c1[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              c0[r] = -fma(zi0[r], e00, zi1[r] * e01);
-              c1[r] = -fma(zi0[r], e01, zi1[r] * e11);
-            }
-            if (br == KR) {
-              c0[KRR] = e00 - 1.0;
-              c1[KRR] = e01;
-              c0[KRR + 1] = e01;
-              c1[KRR + 1] = e11 - 1.0;
-            }
-            if (bc == KT) {   // the pair's columns enter with D - I
-              zr0[KC] -= 1.0;
-              zr1[KC + 1] -= 1.0;
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-              for (int c = 0; c < TW; ++c) W[r][c] = fma(c1[r], zr1[c], fma(c0[r], zr0[c], W[r][c]));
-            if (bc == KT && br == KR) {
-              W[KRR][KC] -= 2.0;
-              W[KRR + 1][KC + 1] -= 2.0;
-            }
-            fsync<LANES>();   // every lane has read the pair's columns before the next are written
-          }
-        });
-      }
-#else
-#pragma unroll 1
-      for (int KT = 0; TW * KT < n; ++KT) {
-        static_for<TW>([&](auto KCc) {
-          constexpr int KC = decltype(KCc)::value;
-          constexpr int KRR = KC & 3;
-          const int K = TW * KT + KC;
-          const int KR = 2 * KT + (KC >> 2);
-          if (K < n) {
-            if (br == KR) {   // row K: columns 8 bc .. 8 bc + 7
-              double rowk[TW];
-#pragma unroll
-              for (int c = 0; c < TW; ++c) rowk[c] = W[KRR][c];
-              stt<TW>(zc, bc, rowk);
-            }
-            if (bc == KT) {   // column K: rows 4 br .. 4 br + 3 (written last: wins on the overlap)
-              d2* pz = reinterpret_cast<d2*>(zc + 4 * br);
-              pz[0] = d2{W[0][KC], W[1][KC]};
-              pz[1] = d2{W[2][KC], W[3][KC]};
-            }
-            fsync<LANES>();
-            double zr[TW], zi[4];
-            ldt<TW>(zr, zc, bc);
-            ld4(zi, zc, br);
-            const double dK = zc[K];
-            const double inv = rcp_nr(dK);
-            double beta[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) beta[r] = -zi[r] * inv;
-            if (br == KR) beta[KRR] = inv - 1.0;
-            if (bc == KT) zr[KC] = dK - 1.0;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-              for (int c = 0; c < TW; ++c) W[r][c] = fma(beta[r], zr[c], W[r][c]);
-            W[KRR][KC] += (bc == KT && br == KR) ? -2.0 : 0.0;
-            fsync<LANES>();   // every lane has read the pivot column before the next is written
-          }
-        });
-      }
-#endif
-      // P = -(sweep result), staged in the second half of ht
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < TW; ++c) sm.ht[2048 + (TW * r + c) * LANES + lane] = -W[r][c];
-    }
-    fsync<NT>();
-    // every lane's full tile (tr, tc) of P: a lower tile directly, an upper one from the
-    // transposed entries of the lower tiles (2 tc + c / 4, tr / 2); rows / columns >= 60 are
-    // the padding's -identity
-    // the same for H (identity padding) back into the full lane-interleaved layout the
-    // drop path reads: its tile rows 2, 3 (full-layout elements 16..31: the staging half)
-    // once every lane holds its P tile, then rows 0, 1 (the lower-tile half)
-    {
-      const bool lower = tc <= (tr >> 1);
-      const int lb = lt_idx(tr < 15 ? tr : 14, tc);
-      const int ub0 = 256 * (tr & 1) + lt_idx(2 * tc, tr >> 1);
-      const int ub1 = 256 * (tr & 1) + lt_idx(2 * tc + 1 < 15 ? 2 * tc + 1 : 14, tr >> 1);
-      auto gaddr = [&](int r, int c) -> int {
-        return lower ? (TW * r + c) * LANES + lb : (TW * (c & 3) + r) * LANES + (c < 4 ? ub0 : ub1);
-      };
-      auto gvalid = [&](int r, int c) -> bool { return lower ? tr < 15 : (c < 4 || tc < 7); };
-      double Hh[2][TW];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < TW; ++c) {
-          const double v = sm.ht[2048 + gaddr(r, c)];
-          W[r][c] = gvalid(r, c) ? v : (4 * tr + r == TW * tc + c ? -1.0 : 0.0);
-        }
-#pragma unroll
-      for (int r = 2; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < TW; ++c) {
-          const double h = sm.ht[gaddr(r, c)];
-          Hh[r - 2][c] = gvalid(r, c) ? h : (4 * tr + r == TW * tc + c ? 1.0 : 0.0);
-        }
-      fsync<NT>();   // the staging half is read
-#pragma unroll
-      for (int r = 2; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < TW; ++c) sm.ht[(TW * r + c) * NT + tid] = Hh[r - 2][c];
-#pragma unroll
-      for (int r = 0; r < 2; ++r)
-#pragma unroll
-        for (int c = 0; c < TW; ++c) {
-          const double h = sm.ht[gaddr(r, c)];
-          Hh[r][c] = gvalid(r, c) ? h : (4 * tr + r == TW * tc + c ? 1.0 : 0.0);
-        }
-      fsync<NT>();   // the lower-tile half is read
-#pragma unroll
-      for (int r = 0; r < 2; ++r)
-#pragma unroll
-        for (int c = 0; c < TW; ++c) sm.ht[(TW * r + c) * NT + tid] = Hh[r][c];
-    }
-  } else if constexpr (kMfmaSweep) {
-    // class 64: blocked by 4 pivots on the f64 matrix cores (mpcqp_sweep_mfma.h),
-    // in the LDS of the H copy, which is stored afterwards
-    double Ws[4][TW];
-    sweep_mfma64(W, Ws, sm.ht, n, tid);
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int c = 0; c < TW; ++c) {
-        sm.ht[(TW * r + c) * NT + tid] = W[r][c];
-        W[r][c] = Ws[r][c];
-      }
-  } else if constexpr (NV >= 96 && MPCQP_SWEEP_PIPE2) {
-  // The pivot-pair pass below, software-pipelined (one robot per CU: the sweep is a
-  // latency chain here, not issue-bound as class 64's four robots are): pair {K, K + 1}
-  // updates the next pair's two register columns at once and defers its other columns
-  // (and the -2 on its diagonal) behind the next pair's barrier, where they issue under
-  // the pivot-column loads and the 2 x 2 inverse.  Each entry takes every pair's FMAs in
-  // pair order: bitwise the same W.
-  double dc0[4], dc1[4], dr0[TW], dr1[TW], dfix = 0.0;
-  int dkrr = 0;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    dc0[r] = 0.0;
-    dc1[r] = 0.0;
-  }
-#pragma unroll
-  for (int c = 0; c < TW; ++c) {
-    dr0[c] = 0.0;
-    dr1[c] = 0.0;
-  }
-  // the -2 on a pair's diagonal (columns kc, kc + 1, rows krr, krr + 1 of the lane holding it)
-  auto pair_fix = [&](auto kcc, int krr, double fx) {
-    constexpr int kc = decltype(kcc)::value;
-    if constexpr (TW == 8) {
-      W[kc & 3][kc] -= fx;
-      W[(kc & 3) + 1][kc + 1] -= fx;
-    } else {
-#pragma unroll
-      for (int r = 0; r < 4; r += 2) {
-        W[r][kc] -= r == krr ? fx : 0.0;
-        W[r + 1][kc + 1] -= r == krr ? fx : 0.0;
-      }
-    }
-  };
-#pragma unroll 1
-  for (int KT = 0; TW * KT < n; ++KT) {
-    static_for<TW / 2>([&](auto KPc) {
-      constexpr int KC = 2 * decltype(KPc)::value;
-      constexpr int KP = (KC + TW - 2) % TW;   // the previous pair's first register column
-      constexpr int KN = (KC + 2) % TW;        // this pair's eager columns KN, KN + 1
-      const int K = TW * KT + KC;
-      const int KR = TW == 8 ? 2 * KT + (KC >> 2) : K >> 2;
-      const int KRR = TW == 8 ? (KC & 3) : (K & 3);   // 0 or 2
-      if (K < n) {
-        double* const z0 = sm.zc[0] + ((K >> 1) & 1) * (2 * C::VEC);
-        double* const z1 = z0 + C::VEC;
-        if (tc == KT) {   // columns KC, KC + 1 took the previous pair eagerly
-          d2* q0 = reinterpret_cast<d2*>(z0 + 4 * tr);
-          q0[0] = d2{W[0][KC], W[1][KC]};
-          q0[1] = d2{W[2][KC], W[3][KC]};
-          d2* q1 = reinterpret_cast<d2*>(z1 + 4 * tr);
-          q1[0] = d2{W[0][KC + 1], W[1][KC + 1]};
-          q1[1] = d2{W[2][KC + 1], W[3][KC + 1]};
-        }
-        fsync<NT>();
-        const double d00 = z0[K], d01 = z0[K + 1], d11 = z1[K + 1];   // first: the inverse waits for these
-        double zr0[TW], zr1[TW], zi0[4], zi1[4];
-        ldt<TW>(zr0, z0, tc);
-        ldt<TW>(zr1, z1, tc);
-        ld4(zi0, z0, tr);
-        ld4(zi1, z1, tr);
-        // the previous pair's deferred columns (all but KC, KC + 1), then its diagonal
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int c = 0; c < TW; ++c)
-            if (c != KC && c != KC + 1) W[r][c] = fma(dc1[r], dr1[c], fma(dc0[r], dr0[c], W[r][c]));
-        pair_fix(std::integral_constant<int, KP>{}, dkrr, dfix);
-        const double idet = rcp_nr(fma(d00, d11, -d01 * d01));
-        const double e00 = d11 * idet, e01 = -d01 * idet, e11 = d00 * idet;   // D^-1
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          dc0[r] = -fma(zi0[r], e00, zi1[r] * e01);
-          dc1[r] = -fma(zi0[r], e01, zi1[r] * e11);
-        }
-        if constexpr (TW == 8) {
-          if (tr == KR) {
-            dc0[KRR] = e00 - 1.0;
-            dc1[KRR] = e01;
-            dc0[KRR + 1] = e01;
-            dc1[KRR + 1] = e11 - 1.0;
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; r += 2) {
-            const bool at = tr == KR && r == KRR;
-            dc0[r] = at ? e00 - 1.0 : dc0[r];
-            dc1[r] = at ? e01 : dc1[r];
-            dc0[r + 1] = at ? e01 : dc0[r + 1];
-            dc1[r + 1] = at ? e11 - 1.0 : dc1[r + 1];
-          }
-        }
-        if (tc == KT) {   // the pair's columns enter with D - I
-          zr0[KC] -= 1.0;
-          zr1[KC + 1] -= 1.0;
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int c = KN; c < KN + 2; ++c) W[r][c] = fma(dc1[r], zr1[c], fma(dc0[r], zr0[c], W[r][c]));
-#pragma unroll
-        for (int c = 0; c < TW; ++c) {
-          dr0[c] = zr0[c];
-          dr1[c] = zr1[c];
-        }
-        dfix = (tc == KT && tr == KR) ? 2.0 : 0.0;
-        dkrr = KRR;
-      }
-    });
-  }
-  {   // the last pair's deferred columns and diagonal (its eager columns: kn, kn + 1)
-    const int kl = ((n - 1) >> 1) << 1;   // the last pair's first pivot
-    const int kc = kl % TW, kn = (kc + 2) % TW;
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int c = 0; c < TW; ++c)
-        if (c != kn && c != kn + 1) W[r][c] = fma(dc1[r], dr1[c], fma(dc0[r], dr0[c], W[r][c]));
-    static_for<TW / 2>([&](auto KPc) {
-      constexpr int KC = 2 * decltype(KPc)::value;
-      if (kc == KC) pair_fix(std::integral_constant<int, KC>{}, dkrr, dfix);
-    });
-  }
-  } else if constexpr (NV >= 96) {
+  if constexpr (NV >= 96) {
   // Classes 96 / 128 (one robot per CU, latency-bound; 6- / 8-wave barriers):
   // pivot PAIRS {K, K + 1} (K even: one tile column, one 4-row group; K + 1 = n is
   // the decoupled identity padding when n is odd).  With Z = W[:, {K, K+1}] and its
@@ -731,67 +387,6 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       }
     });
   }
-  } else if constexpr (TW == 8 && MPCQP_SWEEP_PIPE) {
-  // The single-pivot pass below, software-pipelined: pivot K updates register column
-  // (K + 1) % 8 -- the next pivot's column, published at the top of the next step -- at
-  // once, and defers its other seven columns (and the -2 on its diagonal) into step
-  // K + 1, where those FMAs issue behind the barrier under the pivot-column loads and the
-  // reciprocal instead of ahead of the barrier.  Every entry still takes every pivot's
-  // FMA in pivot order: bitwise the same W.
-  double db[4] = {0.0, 0.0, 0.0, 0.0}, dz[TW], dfix = 0.0;
-#pragma unroll
-  for (int c = 0; c < TW; ++c) dz[c] = 0.0;
-#pragma unroll 1
-  for (int KT = 0; TW * KT < n; ++KT) {
-    static_for<TW>([&](auto KCc) {
-      constexpr int KC = decltype(KCc)::value;
-      constexpr int KP = (KC + TW - 1) % TW;   // the previous pivot's register column
-      constexpr int KN = (KC + 1) % TW;        // this pivot's eager column
-      const int K = TW * KT + KC;
-      const int KR = 2 * KT + (KC >> 2);
-      if (K < n) {
-        double* const zc = sm.zc[KC & 1];
-        if (tc == KT) {   // column KC took pivot K - 1 eagerly
-          d2* pz = reinterpret_cast<d2*>(zc + 4 * tr);
-          pz[0] = d2{W[0][KC], W[1][KC]};
-          pz[1] = d2{W[2][KC], W[3][KC]};
-        }
-        fsync<NT>();
-        const double dK = zc[K];   // first: the reciprocal waits for this load only
-        double zr[TW], zi[4];
-        ldt<TW>(zr, zc, tc);
-        ld4(zi, zc, tr);
-        // pivot K - 1's deferred columns (all but KC), then its diagonal fix-up
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int c = 0; c < TW; ++c)
-            if (c != KC) W[r][c] = fma(db[r], dz[c], W[r][c]);
-        W[KP & 3][KP] += dfix;
-        const double inv = rcp_nr(dK);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) db[r] = -zi[r] * inv;
-        if (tr == KR) db[KC & 3] = inv - 1.0;
-        if (tc == KT) zr[KC] = dK - 1.0;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) W[r][KN] = fma(db[r], zr[KN], W[r][KN]);
-#pragma unroll
-        for (int c = 0; c < TW; ++c) dz[c] = zr[c];
-        dfix = (tc == KT && tr == KR) ? -2.0 : 0.0;
-      }
-    });
-  }
-  {   // the last pivot's deferred columns (its eager column is n % 8)
-    const int kn = n & (TW - 1), kp = (n - 1) & (TW - 1);
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int c = 0; c < TW; ++c)
-        if (c != kn) W[r][c] = fma(db[r], dz[c], W[r][c]);
-#pragma unroll
-    for (int c = 0; c < TW; ++c)
-      if (c == kp) W[c & 3][c] += dfix;
-  }
   } else {
   // pivot K = 8 KT + KC: W_ij -= z_i z_j / d, W_iK = z_i / d, W_KK = -1/d (ends at
   // -H^-1; padding rows/columns >= n never change).  One generic rank-1 pass (the
@@ -848,12 +443,10 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   }
   // P = -(sweep result) = H^-1 ; largest diagonal entry (dependency threshold scale)
   double wd = 0.0;
-  if constexpr (!kSym) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+  for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int c = 0; c < TW; ++c) W[r][c] = -W[r][c];
-  }
+    for (int c = 0; c < TW; ++c) W[r][c] = -W[r][c];
   if constexpr (TW == 8) {
     if (tc == (tr >> 1)) {
       // diagonal entries: column r (even tile row) or 4 + r (odd); blended
@@ -989,7 +582,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   // with the split choice (class 64) wave 1 publishes {p, p2} in one pass-tagged LDS word
   constexpr bool kSplit = MPCQP_SPLIT_CHOICE && NV == 64 && C::NW == 2;
   constexpr bool kEarly = kSplit && MPCQP_EARLY_CHOICE;
-  auto choose1 = [&](int tag_it, int& pc, int& pc2) {
+  auto choose = [&](int tag_it, int& pc, int& pc2) {
     pc = -1;
     pc2 = -1;
 #if MPCQP_F32_KEY
@@ -1072,20 +665,8 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   };
-  auto choose = [&](int tag_it, int& pc, int& pc2) {
-    choose1(tag_it, pc, pc2);
-#if MPCQP_DUP == 2   // diagnostic: the choice twice (same result), to price it on the critical path
-    int qq, qq2;
-    choose1(tag_it, qq, qq2);
-    pc = (qq == pc) ? pc : -1;
-    pc2 = (qq2 == pc2) ? pc2 : -1;
-#endif
-  };
   bool early = false;   // kEarly: wave 1 already holds (and has published) the next choice
   int epc = -1, epc2 = -1;
-  // kDropFuse: the previous pass dropped a slot and left this pass's z / r in its buffers
-  constexpr bool kDropFuse = NV == 64 && VPL == 1 && C::NW == 2 && MPCQP_DROP_FUSE;
-  bool fused = false;
   SEC(0);
   while (true) {
     // pair candidate p2 (another foot-step's most violated row), set on a fresh choice
@@ -1184,13 +765,6 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         // so the uniform (SGPR) coefficients need no per-lane mask: only tile column tA stores
         if (cA == 0) colcombo_u<0, TW>(W, Rm, e0, e1, e2, rlive, zq, rq);
         else colcombo_u<3, TW>(W, Rm, e0, e1, e2, rlive, zq, rq);
-      } else if constexpr (TW == 4) {
-        switch (cA) {
-          case 0: colcombo<0, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-          case 1: colcombo<1, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-          case 2: colcombo<2, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-          default: colcombo<3, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-        }
       } else if constexpr (kAsmCombo) {
         // one computed jump into straight-line cases (mpcqp_combo_asm.h); R's half
         // unconditionally (rows of no active slot are zero; a second, P-only table for those
@@ -1238,37 +812,15 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     double* const vr = sm.vr[buf];
     double* const vz2 = sm.zc[buf];
     double* const vr2 = sm.vr2[buf];
-    if (!(kDropFuse && fused)) {   // after a drop z and r are already in vz / vr (p2 < 0)
     combo_store(c0, tcA, a0, a1, a2, vz, vr);
     if (p2 >= 0) combo_store(c02, tcA2, b0, b1, b2, vz2, vr2);
-#if MPCQP_DUP == 1   // diagnostic: the combos twice (same values), to price them on the critical path
-    {
-      double oz = 0.0;
-      asm volatile("" : "+v"(oz));
-      combo_store(c0, tcA, a0 + oz, a1, a2, vz, vr);
-      if (p2 >= 0) combo_store(c02, tcA2, b0 + oz, b1, b2, vz2, vr2);
-    }
-#endif
     SEC(9);
     fsync<NT>();
-#if MPCQP_DUP == 3   // diagnostic: one more workgroup barrier per pass
-    fsync<NT>();
-#endif
-    }
-    fused = false;
     SEC(2);
     // constraint-row steps zs = A z, slot directions r, variable steps
     double zs[CPL];
 #pragma unroll
     for (int k = 0; k < CPL; ++k) zs[k] = cdot(vz, k);
-#if MPCQP_DUP == 5   // diagnostic: the constraint-row products once more (same values)
-    {
-      double oz = 0.0;
-      asm volatile("" : "+v"(oz));
-#pragma unroll
-      for (int k = 0; k < CPL; ++k) zs[k] = cdot(vz, k) + oz * zs[k];
-    }
-#endif
     double zsp = zs[0];
 #pragma unroll
     for (int k = 1; k < CPL; ++k) zsp = (k == (p >> 6)) ? zs[k] : zsp;
@@ -1384,7 +936,6 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         ldt<TW>(cz2, vz2, tc);
         ld4(z41, vz, tr);
         ld4(z42, vz2, tr);
-#ifndef MPCQP_ABL_NOUPD
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const double al = fma(i11, z41[r], i12 * z42[r]);
@@ -1392,16 +943,6 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
           for (int c = 0; c < TW; ++c) W[r][c] = fma(-be, cz2[c], fma(-al, cz1[c], W[r][c]));
         }
-#if MPCQP_DUP == 6   // diagnostic: P's rank-2 FMAs once more with opaque zero coefficients
-        {
-          double oz = 0.0;
-          asm volatile("" : "+v"(oz));
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int c = 0; c < TW; ++c) W[r][c] = fma(oz, cz2[c], fma(oz, cz1[c], W[r][c]));
-        }
-#endif
         SEC(18);
         if (rlive || slots_live(RPW * wave)) {
           // r / r2 entries read per row (not as two 4-vectors): the shorter live
@@ -1416,16 +957,6 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
             for (int r = 0; r < 4; ++r)
 #pragma unroll
               for (int c = 0; c < TW; ++c) Rm[r][c] = fma(nbe[r], cz2[c], fma(nal[r], cz1[c], Rm[r][c]));
-#if MPCQP_DUP == 7   // diagnostic: R's rank-2 FMAs once more with opaque zero coefficients
-            {
-              double oz = 0.0;
-              asm volatile("" : "+v"(oz));
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int c = 0; c < TW; ++c) Rm[r][c] = fma(oz, cz2[c], fma(oz, cz1[c], Rm[r][c]));
-            }
-#endif
           } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -1439,7 +970,6 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
           }
           }
         }
-#endif
         p = -1;
         CNT(15);
         SEC(0);
@@ -1562,15 +1092,6 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       fsync<NT>();
       const double ie = rcp_nr(sm.yv[l]);
       iedrop = ie;
-      if constexpr (kDropFuse) {
-        // the next pass retries p: z' = P' a_p = z + (r_l / eta) R_l^T and r' = R' a_p =
-        // r - (r_l / eta) y, r'_l = 0 (r_l = R_l . a_p), into its buffers (wave 0 z', wave 1
-        // r'; visible after this pass's closing barrier), instead of its column combinations
-        const double cf = vr[l] * ie;
-        if (wave == 0) sm.vz[buf ^ 1][lane] = fma(cf, sm.rl[lane], vz[lane]);
-        else sm.vr[buf ^ 1][lane] = lane == l ? 0.0 : fma(-cf, sm.yv[lane], vr[lane]);
-        fused = true;
-      }
       double rl4[4], yv4[4];
       ld4(rl4, sm.rl, tr);
       ld4(yv4, sm.yv, tr);
@@ -1586,7 +1107,6 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       occ[l >> 6] &= ~(1ull << (l & 63));
     }
     SEC(13);
-#ifndef MPCQP_ABL_NOUPD
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -1597,7 +1117,6 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
         for (int c = 0; c < TW; ++c) Rm[r][c] = fma(aR[r], cv[c], Rm[r][c]);
     }
-#endif
     if (zrow >= 0) {
       if (kCurKey && (!kSplit || wave == 1)) {   // q_c is read only by the choosing wave
 #pragma unroll

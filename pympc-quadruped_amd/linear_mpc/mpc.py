@@ -62,6 +62,12 @@ def _weight_matrix(W, n, name):
     return W.copy()
 
 
+def _cross_leg(R):
+    """True when R has a nonzero entry between two different legs' 3x3 blocks."""
+    leg = np.arange(12) // 3
+    return bool(np.any(R[leg[:, None] != leg[None, :]] != 0.0))
+
+
 class ModelPredictiveController():
 
     def __init__(self, mpc_config, robot_config):
@@ -90,6 +96,11 @@ class ModelPredictiveController():
         self.com_height_des = robot_config.base_height_des
         self.Q = _weight_matrix(mpc_config.Q, 13, "Q")
         self.R = _weight_matrix(mpc_config.R, 12, "R")
+        if 12 * int(self.horizon) > 128 and _cross_leg(self.R):
+            # 12 N > 128: a standing schedule has n > 128 variables and goes to the
+            # interior-point class, which takes leg-block R only
+            raise ValueError(f"LinearMpcConfig.R couples different legs; at horizon {self.horizon} the "
+                             "engine's interior-point class (n > 128) supports leg-block R only")
         I = np.asarray(self.base_inertia_base, dtype=np.float32)
         self._robot_record = pack_robot(
             dict(mass=float(self.mass), fz_max=float(self.fz_max), mu=float(self.mu),
@@ -334,7 +345,7 @@ class ModelPredictiveController():
         N12 = 12 * self.horizon
         U = out[:N12].astype(np.float64)
         status = int(out[N12:N12 + 1].view(np.int32)[0])
-        if status == 3 or status == 4:   # MPCQP_STATUS_TOO_LARGE / NONFINITE: no usable forces
+        if status in (3, 4, 5):   # TOO_LARGE / NONFINITE / UNSUPPORTED: no iterate, U = 0
             raise RuntimeError(f"mpcqp: robot solve failed with status {status}")
         if status != 0:
             # mpc.py:284-286 never checks is_success; the best iterate is returned, loudly

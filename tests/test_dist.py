@@ -62,7 +62,7 @@ def test_bench_spawns_its_own_ranks(total):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--rehearse-cpu",
-                          "--steps", "3", "--total", str(total)],
+                          "--steps", "3", "--total", str(total), "--no-cpu"],
                          capture_output=True, text=True, timeout=300, env=env, check=True)
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout   # rank 0 only
@@ -91,8 +91,10 @@ def test_bench_rehearsal_world8(config, total):
     want_total = total or world * bpg
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env["OMP_NUM_THREADS"] = "1"
+    # the CPU baseline leg runs once (config 2's 1 024-robot shard); the big shards skip it
+    cpu = ["--cpu-seconds", "0.4"] if config == "config2" else ["--no-cpu"]
     cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", str(world), "--rehearse-cpu",
-           "--config", config, "--steps", "2"] + (["--total", str(total)] if total else [])
+           "--config", config, "--steps", "2"] + (["--total", str(total)] if total else []) + cpu
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, check=True)
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout
@@ -100,3 +102,10 @@ def test_bench_rehearsal_world8(config, total):
     assert line["n_gpus"] == world and line["gathered_rows"] == want_total and line["gather_ok"] is True
     assert line["config"]["global_batch"] == want_total and line["horizon"] == N
     assert line["per_rank_batch"] == [shard(want_total, r, world)[1] for r in range(world)]
+    # the same key set as the measured N = 1 line (tests/test_gpu_dist.py::test_bench_contract_line)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in line, k
+    if config == "config2":
+        c = line["cpu_baseline"]
+        assert c["kind"] == "port" and c["value"] > 0 and c["single_core"]["cores"] == 1 and "rank 0" in c["note"]

@@ -491,3 +491,10 @@ def test_full_weights_cross_leg_r_and_validation():
     assert set_raw(ctypes.c_void_p(0), Q, R) == _lib.ERR_ARG
     again = _solve(eng, bt)   # the previous (valid) weights still in force
     np.testing.assert_array_equal(again[0], u0)
+    # NULL keeps the current matrix whole: (Q_full, R) then (NULL, R) solves as (Q_full, R)
+    null = ctypes.c_void_p(0)
+    assert int(eng.lib.mpcqp_set_weights(eng._ctx, null, np.ascontiguousarray(R).ctypes.data)) == 0
+    kept = _solve(eng, bt)
+    np.testing.assert_array_equal(kept[0], u0)
+    assert int(eng.lib.mpcqp_set_weights(eng._ctx, np.ascontiguousarray(Q).ctypes.data, null)) == 0
+    np.testing.assert_array_equal(_solve(eng, bt)[0], u0)

@@ -174,6 +174,44 @@ def test_shim_takes_full_weights():
     np.testing.assert_array_equal(c.R, LinearMpcConfig.R)
 
 
+def test_shim_rejects_cross_leg_r_beyond_dense_classes():
+    """A cross-leg R entry is accepted at horizon 10 (12 N = 120: every schedule is dense),
+    and rejected at load time at horizon 16, where a standing schedule (n = 192) reaches
+    the interior-point class that takes leg-block R only.  Status 5 from the engine
+    (MPCQP_STATUS_UNSUPPORTED, U = 0) raises instead of returning zero forces."""
+    m = _shim()
+
+    class CrossR(LinearMpcConfig):
+        R = LinearMpcConfig.R.copy()
+    CrossR.R[2, 5] = CrossR.R[5, 2] = 1e-6
+
+    class CrossR16(CrossR):
+        horizon = 16
+
+    class LegBlockR16(LinearMpcConfig):
+        horizon = 16
+        R = LinearMpcConfig.R.copy()
+    LegBlockR16.R[3, 4] = LegBlockR16.R[4, 3] = 1e-6
+
+    m.ModelPredictiveController(CrossR, AliengoConfig)
+    m.ModelPredictiveController(LegBlockR16, AliengoConfig)
+    with pytest.raises(ValueError, match="leg-block R"):
+        m.ModelPredictiveController(CrossR16, AliengoConfig)
+
+    c = m.ModelPredictiveController(LinearMpcConfig, AliengoConfig)
+    class _Out:   # the pinned readback buffer's .numpy()
+        def __init__(self, a):
+            self.a = a
+
+        def numpy(self):
+            return self.a
+    buf = np.zeros(12 * c.horizon + 2, dtype=np.float32)
+    buf[12 * c.horizon:12 * c.horizon + 1].view(np.int32)[0] = 5
+    c._out_pinned = _Out(buf)
+    with pytest.raises(RuntimeError, match="status 5"):
+        c._read_out()
+
+
 def test_engine_weight_split():
     """engine._weights: diagonal input keeps the fast path (full is None); a symmetric
     off-diagonal matrix is passed whole; an asymmetric one raises."""

@@ -25,7 +25,7 @@
 // (free during the sweep: H itself stays in the caller's registers and is stored as
 // the drop path's copy afterwards).
 
-typedef double d4 __attribute__((ext_vector_type(4)));
+// d4: the ext_vector_type(4) double typedef of mpcqp.hip
 
 // On entry W holds H in the 4 x 8 tile layout (lane (tr, tc) = (tid / 8, tid % 8):
 // rows 4 tr .. 4 tr + 3, columns 8 tc .. 8 tc + 7).  On exit Wout holds the sweep

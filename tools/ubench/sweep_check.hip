@@ -3,6 +3,7 @@
 // (when tools/ubench/realH.bin / realR.bin exist: 16 padded 64 x 64 stance-reduced
 // Hessians and numpy's -H^-1, float64) on real config-2 Hessians.
 #include "../../pympc-quadruped_amd/csrc/mpcqp.hip"
+#include "mpcqp_sweep_mfma.h"
 
 #include <stdio.h>
 #include <stdlib.h>
