@@ -52,6 +52,20 @@ static_assert(kMaxN == 20, "the dense classes' and the interior-point class's LD
 #ifndef MPCQP_CURKEY_MAX_NV
 #define MPCQP_CURKEY_MAX_NV 64   // row choice in the current projected metric up to this class
 #endif
+#ifndef MPCQP_C64_ONEWAVE
+// 1: class 64 as ONE wave per robot (4 x 16 register tiles, 512-VGPR budget: one robot per
+// SIMD, four per CU) -- no workgroup barrier in the sweep or the active-set loop
+#define MPCQP_C64_ONEWAVE 0
+#endif
+#ifndef MPCQP_C96_TW
+// class 96's register tile width: 6 (4 x 6 tiles, 6 waves, two waves share two of the four
+// SIMDs) or 12 (4 x 12 tiles, 3 waves, one per SIMD with the 512-VGPR budget)
+#define MPCQP_C96_TW 6
+#endif
+#ifndef MPCQP_C128_TW
+// class 128's register tile width: 8 (8 waves, two per SIMD) or 16 (4 waves, one per SIMD)
+#define MPCQP_C128_TW 8
+#endif
 #ifndef MPCQP_ASM_COMBO
 // class 64's z / r column combination as one computed jump (mpcqp_combo_asm.h) instead of
 // the compiler's branch tree over an 8-way switch
@@ -346,7 +360,7 @@ constexpr int kCap64 = 64;
 // than 64 stance variables are appended to `queue` (when given) for class 96, those
 // with more than 96 to `queue_big` (when given) for class 128.
 template <bool FULL>
-__global__ __launch_bounds__(Cfg<64>::NT) __attribute__((amdgpu_waves_per_eu(2, Cfg<64>::NW))) void mpcqp_kernel_64(
+__global__ __launch_bounds__(Cfg<64>::NT) __attribute__((amdgpu_waves_per_eu(MPCQP_C64_ONEWAVE ? 1 : 2, Cfg<64>::NW))) void mpcqp_kernel_64(
     KParams P, int B, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
@@ -363,7 +377,7 @@ __global__ __launch_bounds__(Cfg<64>::NT) __attribute__((amdgpu_waves_per_eu(2, 
 // stance variables go on to class 128 through `qout`.  Same launch / reset protocol
 // as class 128 below.
 template <bool FULL>
-__global__ __launch_bounds__(Cfg<96>::NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void mpcqp_kernel_96(
+__global__ __launch_bounds__(Cfg<96>::NT) __attribute__((amdgpu_waves_per_eu(MPCQP_C96_TW == 12 ? 1 : 2, MPCQP_C96_TW == 12 ? 1 : 2))) void mpcqp_kernel_96(
     KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
@@ -395,7 +409,12 @@ __global__ __launch_bounds__(Cfg<96>::NT) __attribute__((amdgpu_waves_per_eu(2, 
 // workgroups, queue[4..] = robot indices).  Workloads that fit class 64 skip this
 // launch via mpcqp_set_stance_hint.
 template <bool FULL>
-__global__ __launch_bounds__(Cfg<128>::NT) void mpcqp_kernel_128(
+#if MPCQP_C128_TW == 16
+#define MPCQP_C128_ATTR __attribute__((amdgpu_waves_per_eu(1, 1)))
+#else
+#define MPCQP_C128_ATTR
+#endif
+__global__ __launch_bounds__(Cfg<128>::NT) MPCQP_C128_ATTR void mpcqp_kernel_128(
     KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,

@@ -28,7 +28,7 @@
 template <int NV>
 struct Cfg {
   // tile width: 4 x TW register tiles
-  static constexpr int TW = NV == 96 ? 6 : 8;
+  static constexpr int TW = NV == 96 ? MPCQP_C96_TW : NV == 128 ? MPCQP_C128_TW : (MPCQP_C64_ONEWAVE ? 16 : 8);
   static constexpr int NW = NV * NV / (4 * TW * LANES);   // waves per robot
   static constexpr int NT = NW * LANES;
   static constexpr int TCN = NV / TW;         // tile columns (lanes per tile row)
@@ -37,7 +37,7 @@ struct Cfg {
   static constexpr int VPL = (NV + LANES - 1) / LANES;   // variables / slots per lane
   static constexpr int VEC = VPL * LANES;     // LDS vector length (entries >= NV are padding)
   static_assert(NW * LANES * 4 * TW == NV * NV, "4 x TW tiles");
-  static_assert(TCN == 8 || TCN == 16, "tile rows are reduced over 8 or 16 lanes");
+  static_assert(TCN == 4 || TCN == 8 || TCN == 16, "tile rows are reduced over 4, 8 or 16 lanes");
 };
 
 // Every class keeps a copy of H (its register tiles, lane-interleaved) in LDS for
@@ -101,6 +101,20 @@ __device__ __forceinline__ double dpp_shl1(double v) {
 // 4tr + 2 bit2(lane) + bit1(lane) (see trow / twriter).
 template <int TCN>
 __device__ __forceinline__ double tile_reduce(const double (&acc)[4], int lane) {
+  if constexpr (TCN == 4) {   // one-wave class 64 (4 x 16 tiles): lane keeps row 4tr + (lane & 3)
+    const bool hi2 = (lane & 2) != 0;
+    double k2[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const double send = hi2 ? acc[k] : acc[2 + k];
+      const double keep = hi2 ? acc[2 + k] : acc[k];
+      k2[k] = keep + dpp_d<DPP_XOR2>(send);
+    }
+    const bool hi1 = (lane & 1) != 0;
+    const double send = hi1 ? k2[0] : k2[1];
+    const double keep = hi1 ? k2[1] : k2[0];
+    return keep + dpp_d<DPP_XOR1>(send);
+  }
   const bool hi4 = (lane & 4) != 0;
   double k2[2];
 #pragma unroll
@@ -117,11 +131,14 @@ __device__ __forceinline__ double tile_reduce(const double (&acc)[4], int lane) 
   if constexpr (TCN == 16) y += dpp_d<DPP_ROR8>(y);
   return y;
 }
-__device__ __forceinline__ int trow(int tr, int lane) { return 4 * tr + 2 * ((lane >> 2) & 1) + ((lane >> 1) & 1); }
 template <int TCN>
-__device__ __forceinline__ bool twriter(int lane) { return TCN == 16 ? (lane & 9) == 0 : (lane & 1) == 0; }
+__device__ __forceinline__ int trow(int tr, int lane) {
+  return TCN == 4 ? 4 * tr + (lane & 3) : 4 * tr + 2 * ((lane >> 2) & 1) + ((lane >> 1) & 1);
+}
+template <int TCN>
+__device__ __forceinline__ bool twriter(int lane) { return TCN == 4 ? true : TCN == 16 ? (lane & 9) == 0 : (lane & 1) == 0; }
 
-// y = M v, v in LDS; returns row trow(tr, lane)'s value
+// y = M v, v in LDS; returns row trow<TCN>(tr, lane)'s value
 template <int TCN, int TW>
 __device__ __forceinline__ double tile_matvec4(const double (&M)[4][TW], const double* v, int tc, int lane) {
   double vs[TW];
@@ -481,7 +498,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   // unconstrained minimiser x = -W g
   {
     const double y = tile_matvec4<TCN, TW>(W, sm.gv, tc, lane);
-    if (twriter<TCN>(lane)) sm.vx[trow(tr, lane)] = -y;
+    if (twriter<TCN>(lane)) sm.vx[trow<TCN>(tr, lane)] = -y;
   }
   fsync<NT>();
   double wscale = sm.wmax[0];
@@ -581,7 +598,10 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   // (f32-rounded keys, lowest lane on ties), then the best row of any other foot-step;
   // with the split choice (class 64) wave 1 publishes {p, p2} in one pass-tagged LDS word
   constexpr bool kSplit = MPCQP_SPLIT_CHOICE && NV == 64 && C::NW == 2;
-  constexpr bool kEarly = kSplit && MPCQP_EARLY_CHOICE;
+  // early choice: the choosing wave (wave 1 of the split choice; the only wave of the one-wave
+  // class 64) chooses the next rows before a pass's rank updates, which then overlap it
+  constexpr bool kEarly = (kSplit || (NV == 64 && C::NW == 1)) && MPCQP_EARLY_CHOICE;
+  constexpr int kChooser = C::NW == 1 ? 0 : 1;
   auto choose = [&](int tag_it, int& pc, int& pc2) {
     pc = -1;
     pc2 = -1;
@@ -761,10 +781,19 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     constexpr bool kAsmCombo = (NV == 64 || NV == 128) && TW == 8 && MPCQP_ASM_COMBO;
     auto combo_store = [&](int cA, int tA, double e0, double e1, double e2, double* dz, double* dr) {
       double zq[4], rq[4];
-      if constexpr (TW == 6) {   // foot-steps start at register column 0 or 3: never straddle,
+      if constexpr (TW % 3 == 0) {   // foot-steps start at a register column 3k: never straddle,
         // so the uniform (SGPR) coefficients need no per-lane mask: only tile column tA stores
-        if (cA == 0) colcombo_u<0, TW>(W, Rm, e0, e1, e2, rlive, zq, rq);
-        else colcombo_u<3, TW>(W, Rm, e0, e1, e2, rlive, zq, rq);
+        if constexpr (TW == 6) {
+          if (cA == 0) colcombo_u<0, TW>(W, Rm, e0, e1, e2, rlive, zq, rq);
+          else colcombo_u<3, TW>(W, Rm, e0, e1, e2, rlive, zq, rq);
+        } else {   // TW = 12
+          switch (cA) {
+            case 0: colcombo_u<0, TW>(W, Rm, e0, e1, e2, rlive, zq, rq); break;
+            case 3: colcombo_u<3, TW>(W, Rm, e0, e1, e2, rlive, zq, rq); break;
+            case 6: colcombo_u<6, TW>(W, Rm, e0, e1, e2, rlive, zq, rq); break;
+            default: colcombo_u<9, TW>(W, Rm, e0, e1, e2, rlive, zq, rq); break;
+          }
+        }
       } else if constexpr (kAsmCombo) {
         // one computed jump into straight-line cases (mpcqp_combo_asm.h); R's half
         // unconditionally (rows of no active slot are zero; a second, P-only table for those
@@ -792,10 +821,24 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
           case 4: colcombo<4, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
           case 5: colcombo<5, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
           case 6: colcombo<6, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-          default: colcombo<7, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+          case 7: colcombo<7, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+          default:
+            if constexpr (TW == 16) {
+              switch (cA) {
+                case 8: colcombo<8, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+                case 9: colcombo<9, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+                case 10: colcombo<10, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+                case 11: colcombo<11, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+                case 12: colcombo<12, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+                case 13: colcombo<13, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+                case 14: colcombo<14, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+                default: colcombo<15, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+              }
+            }
+            break;
         }
       }
-      if (TW != 6 && !kAsmCombo && __builtin_expect(cA + 2 >= TW, 0)) {   // straddles tile columns tA, tA + 1
+      if (TW % 3 != 0 && !kAsmCombo && __builtin_expect(cA + 2 >= TW, 0)) {   // straddles tile columns tA, tA + 1
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           zq[r] += dpp_shl1(zq[r]);
@@ -922,7 +965,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         };
         ++it;   // a pair step counts as the two additions it makes
         if constexpr (kEarly) {
-          if (wave == 1) {   // the row values are final for this pass: choose now, before the FMAs
+          if (wave == kChooser) {   // the row values are final for this pass: choose now, before the FMAs
             qm_pair();
             choose(it, epc, epc2);
             early = true;
@@ -1049,7 +1092,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       for (int k = 0; k < CPL; ++k) s[k] = (lane + LANES * k == p) ? 0.0 : s[k];
       p = -1;
       if constexpr (kEarly) {
-        if (wave == 1) {   // the row values are final for this pass: choose before the FMAs
+        if (wave == kChooser) {   // the row values are final for this pass: choose before the FMAs
           if constexpr (kCurKey)   // q_c is read only by the choosing wave
 #pragma unroll
             for (int k = 0; k < CPL; ++k) qm[k] = (float)fma(-zs[k] * zs[k], is, (double)qm[k]);
@@ -1082,12 +1125,12 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
           acc[r] = a + a2;
         }
         const double tvv = tile_reduce<TCN>(acc, lane);
-        if (twriter<TCN>(lane)) sm.tv[trow(tr, lane)] = tvv;
+        if (twriter<TCN>(lane)) sm.tv[trow<TCN>(tr, lane)] = tvv;
       }
       fsync<NT>();
       {
         const double yvv = tile_matvec4<TCN, TW>(Rm, sm.tv, tc, lane);
-        if (twriter<TCN>(lane)) sm.yv[trow(tr, lane)] = yvv;
+        if (twriter<TCN>(lane)) sm.yv[trow<TCN>(tr, lane)] = yvv;
       }
       fsync<NT>();
       const double ie = rcp_nr(sm.yv[l]);
