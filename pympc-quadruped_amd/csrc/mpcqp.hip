@@ -31,6 +31,7 @@
 
 #include <new>
 #include <string>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -442,23 +443,23 @@ __global__ __launch_bounds__(Cfg<128>::NT) MPCQP_C128_ATTR void mpcqp_kernel_128
 // Large class (n > 128: standing schedules at N >= 11): one wave per queued robot,
 // Riccati-factored interior point + active-set polish (mpcqp_ipm.h).  Same launch /
 // reset protocol as class 128.  FULL: non-diagonal weights (mpcqp_set_weights).
-template <bool FULL>
+template <bool FULL, int NM>
 __global__ __launch_bounds__(LANES) void mpcqp_kernel_ipm(
     KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
     int* __restrict__ queue, int direct_B) {
-  __shared__ IpmShared sm;
+  __shared__ IpmSharedT<NM> sm;
   const int tid = threadIdx.x;
   const int k = blockIdx.x;
   if (direct_B > 0) {
-    if (k < direct_B) solve_robot_ipm<FULL>(P, k, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg);
+    if (k < direct_B) solve_robot_ipm<FULL, NM>(P, k, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg);
     return;
   }
   const int cnt = uni(__hip_atomic_load(&queue[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   if (k < cnt) {
     const int b = uni(queue[4 + k]);
-    solve_robot_ipm<FULL>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg);
+    solve_robot_ipm<FULL, NM>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg);
     if (tid == 0 && atomicAdd(&queue[2], 1) == cnt - 1) {
       atomicExch(&queue[0], 0);
       atomicExch(&queue[2], 0);
@@ -710,7 +711,10 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   const bool fork = giant && first < 3 && side_stream(qs);
   bool ipm_done = false;
   auto launch_ipm = [&](hipStream_t s) -> hipError_t {
-    hipLaunchKernelGGL(full ? mpcqp_kernel_ipm<true> : mpcqp_kernel_ipm<false>, dim3(batch), dim3(LANES), 0, s, kp, x0, xref, contact, feet, robot, u0, U,
+    // N <= 16 (the reference's default horizon): the 16-stage LDS layout, two robots per CU
+    auto kern = kp.N <= 16 ? (full ? mpcqp_kernel_ipm<true, 16> : mpcqp_kernel_ipm<false, 16>)
+                        : (full ? mpcqp_kernel_ipm<true, kMaxN> : mpcqp_kernel_ipm<false, kMaxN>);
+    hipLaunchKernelGGL(kern, dim3(batch), dim3(LANES), 0, s, kp, x0, xref, contact, feet, robot, u0, U,
                        (int*)status, (int*)iters, q + 2 * (4 + (size_t)cap), first == 3 ? (int)batch : 0);
     ipm_done = true;
     return hipGetLastError();

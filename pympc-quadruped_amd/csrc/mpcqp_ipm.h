@@ -44,53 +44,71 @@ constexpr double IPM_POLISH_MU = MPCQP_IPM_POLISH_MU;
 constexpr double IPM_MU_FLOOR = 1e-13;
 constexpr double IPM_STAT_TOL = 1e-10;
 constexpr int IPM_FPL = 2;             // stance foot-steps per lane (4 kMaxN <= 128)
-constexpr int IPM_NF = 4 * kMaxN;
 
-struct alignas(16) IpmShared {
+// per stance foot-step interior-point state (row slots 0..5)
+template <int NF>
+struct IpmFootLds {
+  double fs[NF][6], fl[NF][6], frp[NF][6], frd[NF][4];
+  union {
+    struct {
+      double fds[NF][6], fdl[NF][6];   // Newton directions of s and lambda
+    };
+    double fpj[NF][9];             // polish: null-space projector per foot-step
+  };
+  int fact[NF];                    // polish: active rows per foot-step
+  int fprev[NF];                   // polish: the rows of the previous try
+};
+struct IpmFootNone {};
+// the same for the one foot-step of a lane (registers)
+struct IpmFootReg {
+  double fs[6], fl[6], frp[6], frd[4], fds[6], fdl[6], fpj[9];
+  int fact, fprev;
+};
+
+// LDS of one robot, sized for horizons N <= NM: NM = 16 (the reference's default horizon)
+// takes 79 KB -- two robots per CU --, NM = 20 one robot per CU
+template <int NM>
+struct alignas(16) IpmSharedT {
+  static constexpr int IPM_NF = 4 * NM;
   union {
     struct {
       Form f;
       FormY fy;
     } fa;                          // formulation scratch (dead once Bm / x0 / xr are copied)
-    alignas(16) double S[kMaxN][144];   // Riccati S_k (12 x 12, row-major, symmetric)
+    struct {
+      alignas(16) double S[NM][144];   // Riccati S_k (12 x 12, row-major, symmetric)
+      alignas(16) double M[NM][144];   // M_k = A^T (I - S_k E_k): lsolve's stage maps (row-major)
+    };
   };
   RobotMeta mt;
   alignas(16) double Bm[12][12];   // B_d rows 0..11 (row 12 is 0)
   alignas(16) double BmT[12][12];  // its transpose
   alignas(16) double TT[12][12];   // factor scratch: (I + P E)^T, then S_k^T
-  alignas(16) double M[kMaxN][144];   // M_k = A^T (I - S_k E_k): lsolve's stage maps (row-major)
   double nmr[3][3];                // h R_z^T: A_d[r][6 + c] (r < 3)
   double x0[16];
-  double xr[kMaxN][NX];            // xref, float64
+  double xr[NM][NX];            // xref, float64
   double qh[16];                   // 2 q
   double rh[NU];                   // 2 r
   double qf[NX][NX];               // Qh = 2 Q (full; the diagonal case fills the diagonal)
   double rf[NU][NU];               // Rh = 2 R (leg blocks used)
   double W[IPM_NF][9];             // per stance foot-step 3x3 weight of the Newton system
   alignas(16) double P[144];       // P_{k+1}
-  alignas(16) double U[kMaxN][NU]; // iterate (swing entries 0)
-  alignas(16) double dU[kMaxN][NU];
-  alignas(16) double rhs[kMaxN][NU];
-  alignas(16) double gr[kMaxN][NU];
-  alignas(16) double Y[kMaxN][NU];
-  alignas(16) double By[kMaxN][NU];
-  alignas(16) double Us[kMaxN][NU];   // the IPM iterate while a polish overwrites U
-  alignas(16) double X[kMaxN + 1][16];
-  alignas(16) double BU[kMaxN][NU];   // gradient: B_d U_k
-  alignas(16) double nuh[kMaxN][NU];  // gradient: adjoint nu_k (rows 0..11)
-  alignas(16) double la[kMaxN][NU], lb[kMaxN][NU], lc[kMaxN][NU];   // lsolve: per-stage vectors
-  alignas(16) double ph[kMaxN][NU];   // lsolve: p_{k+1}, the backward recursion's input at stage k
-  alignas(16) double dxh[kMaxN][NU];  // lsolve: dx_k
-  // per stance foot-step interior-point state (row slots 0..5)
-  double fs[IPM_NF][6], fl[IPM_NF][6], frp[IPM_NF][6], frd[IPM_NF][4];
-  union {
-    struct {
-      double fds[IPM_NF][6], fdl[IPM_NF][6];   // Newton directions of s and lambda
-    };
-    double fpj[IPM_NF][9];         // polish: null-space projector per foot-step
-  };
-  int fact[IPM_NF];                // polish: active rows per foot-step
-  int fprev[IPM_NF];               // polish: the rows of the previous try
+  alignas(16) double U[NM][NU]; // iterate (swing entries 0)
+  alignas(16) double dU[NM][NU];
+  alignas(16) double rhs[NM][NU];
+  alignas(16) double gr[NM][NU];
+  alignas(16) double Y[NM][NU];
+  alignas(16) double By[NM][NU];
+  alignas(16) double Us[NM][NU];   // the IPM iterate while a polish overwrites U
+  alignas(16) double X[NM + 1][16];
+  alignas(16) double BU[NM][NU];   // gradient: B_d U_k
+  alignas(16) double nuh[NM][NU];  // gradient: adjoint nu_k (rows 0..11)
+  alignas(16) double la[NM][NU], lb[NM][NU], lc[NM][NU];   // lsolve: per-stage vectors
+  alignas(16) double ph[NM][NU];   // lsolve: p_{k+1}, the backward recursion's input at stage k
+  alignas(16) double dxh[NM][NU];  // lsolve: dx_k
+  // per stance foot-step interior-point state in LDS when a lane owns more than one
+  // foot-step (NM > 16); with at most 64 foot-steps each lane keeps its one in registers
+  std::conditional_t<(IPM_NF > LANES), IpmFootLds<IPM_NF>, IpmFootNone> ft;
 };
 
 // 12 consecutive doubles of a 16-B aligned LDS vector, 16 B per read
@@ -136,8 +154,8 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 }
 
 // One robot with more than 128 stance variables.  Called by a 64-thread workgroup.
-template <bool FULL>
-__device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmShared& sm,
+template <bool FULL, int NM>
+__device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSharedT<NM>& sm,
                                                 const float* __restrict__ x0g, const float* __restrict__ xrefg,
                                                 const float* __restrict__ contactg, const float* __restrict__ feetg,
                                                 const float* __restrict__ robotg, float* __restrict__ u0g,
@@ -223,6 +241,19 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     o[2] = p[2];
   };
   auto foot_ptr = [&](int j, double (*A)[NU]) -> double* { return &A[sm.mt.foot_t[j]][3 * sm.mt.foot_leg[j]]; };
+  // the lane's stance foot-step state: registers when a lane owns at most one foot-step
+  // (every loop below runs j = lane, lane + 64, ...: then only j = lane), else LDS
+  constexpr bool kRegFoot = 4 * NM <= LANES;
+  IpmFootReg fr;
+  auto FS = [&](int j) -> double (&)[6] { if constexpr (kRegFoot) return fr.fs; else return sm.ft.fs[j]; };
+  auto FL = [&](int j) -> double (&)[6] { if constexpr (kRegFoot) return fr.fl; else return sm.ft.fl[j]; };
+  auto FRP = [&](int j) -> double (&)[6] { if constexpr (kRegFoot) return fr.frp; else return sm.ft.frp[j]; };
+  auto FRD = [&](int j) -> double (&)[4] { if constexpr (kRegFoot) return fr.frd; else return sm.ft.frd[j]; };
+  auto FDS = [&](int j) -> double (&)[6] { if constexpr (kRegFoot) return fr.fds; else return sm.ft.fds[j]; };
+  auto FDL = [&](int j) -> double (&)[6] { if constexpr (kRegFoot) return fr.fdl; else return sm.ft.fdl[j]; };
+  auto FPJ = [&](int j) -> double (&)[9] { if constexpr (kRegFoot) return fr.fpj; else return sm.ft.fpj[j]; };
+  auto FACT = [&](int j) -> int& { if constexpr (kRegFoot) return fr.fact; else return sm.ft.fact[j]; };
+  auto FPREV = [&](int j) -> int& { if constexpr (kRegFoot) return fr.fprev; else return sm.ft.fprev[j]; };
   constexpr int kRh = FULL ? 9 : 3;   // the leg's 3 x 3 block of Rh, or its diagonal
   auto legrh = [&](int j, double (&o)[kRh]) {
     const int l = sm.mt.foot_leg[j];
@@ -701,8 +732,8 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
       const bool on = (liv >> r) & 1;
-      sm.fs[j][r] = on ? fmax(adot(r, f) - (r == 5 ? h5 : 0.0), 1.0) : 1.0;
-      sm.fl[j][r] = on ? 1.0 : 0.0;
+      FS(j)[r] = on ? fmax(adot(r, f) - (r == 5 ? h5 : 0.0), 1.0) : 1.0;
+      FL(j)[r] = on ? 1.0 : 0.0;
     }
   }
   fsync<NT>();
@@ -712,11 +743,11 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     for (int j = lane; j < S; j += NT) {
       double rh[kRh], pj[9], fp[3], wv[9];
       legrh(j, rh);
-      ipm_foot_nullspace(rw, sm.fact[j] & liv, -sm.mt.ub[j], rh, pj, fp, wv);
+      ipm_foot_nullspace(rw, FACT(j) & liv, -sm.mt.ub[j], rh, pj, fp, wv);
 #pragma unroll
       for (int e = 0; e < 9; ++e) {
         sm.W[j][e] = wv[e];
-        sm.fpj[j][e] = pj[e];
+        FPJ(j)[e] = pj[e];
       }
       double* u = foot_ptr(j, sm.U);
       u[0] = fp[0];
@@ -733,7 +764,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       for (int j = lane; j < S; j += NT) {
         double g[3];
         foot(j, sm.gr, g);
-        const double* pj = sm.fpj[j];
+        const double (&pj)[9] = FPJ(j);
         double* r = foot_ptr(j, sm.rhs);
 #pragma unroll
         for (int x = 0; x < 3; ++x) r[x] = -(pj[3 * x] * g[0] + pj[3 * x + 1] * g[1] + pj[3 * x + 2] * g[2]);
@@ -756,7 +787,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       double g[3], f[3];
       foot(j, sm.gr, g);
       foot(j, sm.U, f);
-      const double* pj = sm.fpj[j];
+      const double (&pj)[9] = FPJ(j);
 #pragma unroll
       for (int x = 0; x < 3; ++x) stat = fmax(stat, fabs(pj[3 * x] * g[0] + pj[3 * x + 1] * g[1] + pj[3 * x + 2] * g[2]));
       int viol = 0;
@@ -768,7 +799,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
           smin = fmin(smin, sl);
           if (sl < -tol_h) viol |= 1 << r;
         }
-      const int am = sm.fact[j] & liv;
+      const int am = FACT(j) & liv;
       double best = INFINITY;
       int drop = -1;
       if (am) {
@@ -778,7 +809,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
         ipm_cone_multipliers(rw, am, nq, g, tol_g, best, drop);
       }
       lminw = fmin(lminw, best);
-      sm.fact[j] = (sm.fact[j] | viol) & ~(drop >= 0 ? (1 << drop) : 0);
+      FACT(j) = (FACT(j) | viol) & ~(drop >= 0 ? (1 << drop) : 0);
     }
     stat = wave_max_d(stat);
     smin = wave_min(smin);
@@ -809,14 +840,14 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       for (int x = 0; x < 3; ++x) {
         double v = g[x];
 #pragma unroll
-        for (int r = 0; r < 6; ++r) v = fma(-sm.fl[j][r], rw[r][x], v);
-        sm.frd[j][x] = v;
+        for (int r = 0; r < 6; ++r) v = fma(-FL(j)[r], rw[r][x], v);
+        FRD(j)[x] = v;
       }
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
         const bool on = (liv >> r) & 1;
-        sm.frp[j][r] = on ? adot(r, f) - (r == 5 ? h5 : 0.0) - sm.fs[j][r] : 0.0;
-        sl += on ? sm.fs[j][r] * sm.fl[j][r] : 0.0;
+        FRP(j)[r] = on ? adot(r, f) - (r == 5 ? h5 : 0.0) - FS(j)[r] : 0.0;
+        sl += on ? FS(j)[r] * FL(j)[r] : 0.0;
       }
     }
     const double mu = sgpr_d(wave_sum_d(sl)) / m_tot;
@@ -835,22 +866,22 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
         int a = 0;
 #pragma unroll
         for (int r = 0; r < 6; ++r)
-          if (((liv >> r) & 1) && sm.fl[j][r] > sm.fs[j][r]) a |= 1 << r;
-        sm.fact[j] = a;
+          if (((liv >> r) & 1) && FL(j)[r] > FS(j)[r]) a |= 1 << r;
+        FACT(j) = a;
       }
       // U is overwritten by the polish: keep the IPM iterate
       for (int e = lane; e < N * NU; e += NT) sm.Us[e / NU][e % NU] = sm.U[e / NU][e % NU];
       fsync<NT>();
       for (int corr = 0; corr <= IPM_NCORR; ++corr) {
         int changed = 0;
-        for (int j = lane; j < S; j += NT) sm.fprev[j] = sm.fact[j];
+        for (int j = lane; j < S; j += NT) FPREV(j) = FACT(j);
         fsync<NT>();
         if (polish()) {
           done = true;
           status = MPCQP_STATUS_OK;
           break;
         }
-        for (int j = lane; j < S; j += NT) changed |= sm.fact[j] != sm.fprev[j];
+        for (int j = lane; j < S; j += NT) changed |= FACT(j) != FPREV(j);
         if (!__any(changed)) break;
       }
       if (done) break;
@@ -860,7 +891,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     for (int j = lane; j < S; j += NT) {
       double d[6], rh[kRh], wv[9];
 #pragma unroll
-      for (int r = 0; r < 6; ++r) d[r] = ((liv >> r) & 1) ? sm.fl[j][r] / sm.fs[j][r] : 0.0;
+      for (int r = 0; r < 6; ++r) d[r] = ((liv >> r) & 1) ? FL(j)[r] / FS(j)[r] : 0.0;
       legrh(j, rh);
       ipm_foot_weight(rw, liv, d, rh, wv);
 #pragma unroll
@@ -878,13 +909,13 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
         double* rr = foot_ptr(j, sm.rhs);
 #pragma unroll
         for (int x = 0; x < 3; ++x) {
-          double v = -sm.frd[j][x];
+          double v = -FRD(j)[x];
 #pragma unroll
           for (int r = 0; r < 6; ++r)
             if ((liv >> r) & 1) {
-              const double s_ = sm.fs[j][r], l_ = sm.fl[j][r];
-              const double rc = -s_ * l_ + (corr ? target - sm.fds[j][r] * sm.fdl[j][r] : 0.0);
-              v = fma(rw[r][x], rc / s_ - (l_ / s_) * sm.frp[j][r], v);
+              const double s_ = FS(j)[r], l_ = FL(j)[r];
+              const double rc = -s_ * l_ + (corr ? target - FDS(j)[r] * FDL(j)[r] : 0.0);
+              v = fma(rw[r][x], rc / s_ - (l_ / s_) * FRP(j)[r], v);
             }
           rr[x] = v;
         }
@@ -898,12 +929,12 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
 #pragma unroll
         for (int r = 0; r < 6; ++r)
           if ((liv >> r) & 1) {
-            const double s_ = sm.fs[j][r], l_ = sm.fl[j][r];
-            const double rc = -s_ * l_ + (corr ? target - sm.fds[j][r] * sm.fdl[j][r] : 0.0);
-            const double ds = adot(r, d) + sm.frp[j][r];
+            const double s_ = FS(j)[r], l_ = FL(j)[r];
+            const double rc = -s_ * l_ + (corr ? target - FDS(j)[r] * FDL(j)[r] : 0.0);
+            const double ds = adot(r, d) + FRP(j)[r];
             const double dl = (rc - l_ * ds) / s_;
-            sm.fds[j][r] = ds;
-            sm.fdl[j][r] = dl;
+            FDS(j)[r] = ds;
+            FDL(j)[r] = dl;
             if (ds < 0.0) a1 = fmin(a1, -s_ / ds);
             if (dl < 0.0) a2 = fmin(a2, -l_ / dl);
           }
@@ -915,7 +946,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     for (int j = lane; j < S; j += NT)
 #pragma unroll
       for (int r = 0; r < 6; ++r)
-        if ((liv >> r) & 1) sa += (sm.fs[j][r] + al[0] * sm.fds[j][r]) * (sm.fl[j][r] + al[1] * sm.fdl[j][r]);
+        if ((liv >> r) & 1) sa += (FS(j)[r] + al[0] * FDS(j)[r]) * (FL(j)[r] + al[1] * FDL(j)[r]);
     const double mu_aff = sgpr_d(wave_sum_d(sa)) / m_tot;
     const double sig = mu_aff / mu;
     const double target = fmax(sig * sig * sig * mu, IPM_MU_FLOOR * gscale * hscale);
@@ -932,8 +963,8 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
 #pragma unroll
       for (int r = 0; r < 6; ++r)
         if ((liv >> r) & 1) {
-          sm.fs[j][r] += ap * sm.fds[j][r];
-          sm.fl[j][r] += ad * sm.fdl[j][r];
+          FS(j)[r] += ap * FDS(j)[r];
+          FL(j)[r] += ad * FDL(j)[r];
         }
     }
     fsync<NT>();
