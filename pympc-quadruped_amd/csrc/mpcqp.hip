@@ -354,8 +354,10 @@ __device__ __forceinline__ int xcd_robot(int bid, int B) {
   return x * q + (x < r ? x : r) + i;
 }
 
-// class 64's capacity (stance variables): 60 with the one-wave symmetric sweep
+// class 64's capacity (stance variables)
 constexpr int kCap64 = 64;
+// interior-point class: persistent workgroups per CU (three robots fit a CU's LDS at N <= 16)
+constexpr int kIpmPerCU = 4;
 
 // Class NV = 64: one 2-wave workgroup per robot of the batch.  Robots with more
 // than 64 stance variables are appended to `queue` (when given) for class 96, those
@@ -378,7 +380,7 @@ __global__ __launch_bounds__(Cfg<64>::NT) __attribute__((amdgpu_waves_per_eu(MPC
 // stance variables go on to class 128 through `qout`.  Same launch / reset protocol
 // as class 128 below.
 template <bool FULL>
-__global__ __launch_bounds__(Cfg<96>::NT) __attribute__((amdgpu_waves_per_eu(MPCQP_C96_TW == 12 ? 1 : 2, MPCQP_C96_TW == 12 ? 1 : 2))) void mpcqp_kernel_96(
+__global__ __launch_bounds__(Cfg<96>::NT) __attribute__((amdgpu_waves_per_eu((Cfg<96>::NW + 3) / 4, (Cfg<96>::NW + 3) / 4))) void mpcqp_kernel_96(
     KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
@@ -448,22 +450,30 @@ __global__ __launch_bounds__(LANES) void mpcqp_kernel_ipm(
     KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
-    int* __restrict__ queue, int direct_B) {
+    int* __restrict__ queue, int direct_B, double* __restrict__ sscratch) {
   __shared__ IpmSharedT<NM> sm;
   const int tid = threadIdx.x;
-  const int k = blockIdx.x;
-  if (direct_B > 0) {
-    if (k < direct_B) solve_robot_ipm<FULL, NM>(P, k, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg);
-    return;
+  // persistent workgroups (its global S_k slot is the workgroup's) taking robots by ticket
+  // (queue[1]): a workgroup that finishes early takes the next robot, whatever the residency.
+  // The last workgroup to run out of tickets (queue[3] counts them) resets the queue header
+  // for the next launch -- only then can no workgroup still take a ticket.
+  double* const Sg = sscratch + (size_t)blockIdx.x * IPM_S_SLOT;
+  // direct_B > 0: the caller's stance range rules the dense classes out, ticket = robot
+  const bool direct = direct_B > 0;
+  const int cnt = direct ? direct_B : uni(__hip_atomic_load(&queue[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (cnt == 0) return;   // nothing queued: no counter is touched, none needs a reset
+  while (true) {
+    int t = 0;
+    if (tid == 0) t = atomicAdd(&queue[1], 1);
+    t = __builtin_amdgcn_readlane(t, 0);
+    if (t >= cnt) break;
+    const int b = direct ? t : uni(queue[4 + t]);
+    solve_robot_ipm<FULL, NM>(P, b, sm, Sg, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg);
   }
-  const int cnt = uni(__hip_atomic_load(&queue[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  if (k < cnt) {
-    const int b = uni(queue[4 + k]);
-    solve_robot_ipm<FULL, NM>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg);
-    if (tid == 0 && atomicAdd(&queue[2], 1) == cnt - 1) {
-      atomicExch(&queue[0], 0);
-      atomicExch(&queue[2], 0);
-    }
+  if (tid == 0 && atomicAdd(&queue[3], 1) == (int)gridDim.x - 1) {
+    atomicExch(&queue[0], 0);
+    atomicExch(&queue[1], 0);
+    atomicExch(&queue[3], 0);
   }
 }
 
@@ -483,6 +493,8 @@ struct QueueSet {
   // (routing) class and joined back at the end of the call (created on first use)
   hipStream_t side;
   hipEvent_t ev_fork, ev_join;
+  double* sscratch;   // the interior-point class's Riccati S_k, one slot per workgroup (first use)
+  int sslots;
 };
 
 // Releases a queue set's device resources (the caller has synchronised the device).
@@ -491,6 +503,9 @@ static void release_set(QueueSet& q) {
   if (q.ev_fork) (void)hipEventDestroy(q.ev_fork);
   if (q.ev_join) (void)hipEventDestroy(q.ev_join);
   if (q.side) (void)hipStreamDestroy(q.side);
+  if (q.sscratch) (void)hipFree(q.sscratch);
+  q.sscratch = nullptr;
+  q.sslots = 0;
   q.buf = nullptr;
   q.ev_fork = q.ev_join = nullptr;
   q.side = nullptr;
@@ -557,11 +572,11 @@ static QueueSet* stream_queues(mpcqp_ctx* ctx, hipStream_t st, int batch, int* e
       return nullptr;
     }
     release_set(*lru);
-    *lru = QueueSet{st, 0, nullptr, ++ctx->use_clock, nullptr, nullptr, nullptr};
+    *lru = QueueSet{st, 0, nullptr, ++ctx->use_clock, nullptr, nullptr, nullptr, nullptr, 0};
     qs = lru;
   }
   if (!qs) {
-    ctx->queues.push_back(QueueSet{st, 0, nullptr, ++ctx->use_clock, nullptr, nullptr, nullptr});
+    ctx->queues.push_back(QueueSet{st, 0, nullptr, ++ctx->use_clock, nullptr, nullptr, nullptr, nullptr, 0});
     qs = &ctx->queues.back();
   }
   if (qs->buf) {
@@ -705,17 +720,29 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
     if (!qs) return qerr;
     q = qs->buf;
   }
+  if (giant && !qs->sscratch) {   // the interior-point class's global S_k slots (first use)
+    const int slots = kIpmPerCU * ctx->ncu;
+    if (hipMalloc(&qs->sscratch, sizeof(double) * IPM_S_SLOT * (size_t)slots) != hipSuccess) {
+      qs->sscratch = nullptr;
+      return set_err(ctx, MPCQP_ERR_ALLOC, "interior-point scratch allocation failed");
+    }
+    qs->sslots = slots;
+  }
   // the interior-point class (one wave per robot, latency-bound) on a side stream as soon
   // as the first class has routed its robots, beside classes 96 / 128 instead of behind
   // them; the caller's stream waits for it at the end of the call
   const bool fork = giant && first < 3 && side_stream(qs);
   bool ipm_done = false;
   auto launch_ipm = [&](hipStream_t s) -> hipError_t {
-    // N <= 16 (the reference's default horizon): the 16-stage LDS layout, two robots per CU
+    // N <= 16 (the reference's default horizon): the 16-stage LDS layout, three robots per CU
     auto kern = kp.N <= 16 ? (full ? mpcqp_kernel_ipm<true, 16> : mpcqp_kernel_ipm<false, 16>)
                         : (full ? mpcqp_kernel_ipm<true, kMaxN> : mpcqp_kernel_ipm<false, kMaxN>);
-    hipLaunchKernelGGL(kern, dim3(batch), dim3(LANES), 0, s, kp, x0, xref, contact, feet, robot, u0, U,
-                       (int*)status, (int*)iters, q + 2 * (4 + (size_t)cap), first == 3 ? (int)batch : 0);
+    // persistent workgroups (robots w, w + grid, ...): at most kIpmPerCU per CU, each with a
+    // global S_k slot
+    const int grid = (int)std::min<long long>(batch, (long long)kIpmPerCU * ctx->ncu);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(LANES), 0, s, kp, x0, xref, contact, feet, robot, u0, U,
+                       (int*)status, (int*)iters, q + 2 * (4 + (size_t)cap), first == 3 ? (int)batch : 0,
+                       qs->sscratch);
     ipm_done = true;
     return hipGetLastError();
   };

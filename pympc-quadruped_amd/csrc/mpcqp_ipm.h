@@ -66,7 +66,10 @@ struct IpmFootReg {
 };
 
 // LDS of one robot, sized for horizons N <= NM: NM = 16 (the reference's default horizon)
-// takes 79 KB -- two robots per CU --, NM = 20 one robot per CU
+// takes 52 KB -- three robots per CU --, NM = 20 one robot per CU.  The Riccati S_k live in
+// a per-workgroup global scratch slot (read only by lsolve's batched phases); the
+// formulation scratch shares its space with M_k and the gradient's / lsolve's per-stage
+// temporaries, which are first written after it is dead.
 template <int NM>
 struct alignas(16) IpmSharedT {
   static constexpr int IPM_NF = 4 * NM;
@@ -76,8 +79,21 @@ struct alignas(16) IpmSharedT {
       FormY fy;
     } fa;                          // formulation scratch (dead once Bm / x0 / xr are copied)
     struct {
-      alignas(16) double S[NM][144];   // Riccati S_k (12 x 12, row-major, symmetric)
       alignas(16) double M[NM][144];   // M_k = A^T (I - S_k E_k): lsolve's stage maps (row-major)
+      union {
+        struct {                       // gradient() temporaries
+          alignas(16) double X[NM + 1][16];
+          alignas(16) double BU[NM][NU];   // B_d U_k
+          alignas(16) double nuh[NM][NU];  // adjoint nu_k (rows 0..11)
+        };
+        struct {                       // lsolve() temporaries
+          alignas(16) double Y[NM][NU];
+          alignas(16) double By[NM][NU];
+          alignas(16) double la[NM][NU], lb[NM][NU], lc[NM][NU];   // per-stage vectors
+          alignas(16) double ph[NM][NU];   // p_{k+1}, the backward recursion's input at stage k
+          alignas(16) double dxh[NM][NU];  // dx_k
+        };
+      };
     };
   };
   RobotMeta mt;
@@ -86,30 +102,24 @@ struct alignas(16) IpmSharedT {
   alignas(16) double TT[12][12];   // factor scratch: (I + P E)^T, then S_k^T
   double nmr[3][3];                // h R_z^T: A_d[r][6 + c] (r < 3)
   double x0[16];
-  double xr[NM][NX];            // xref, float64
+  double xr[NM][NX];               // xref, float64
   double qh[16];                   // 2 q
   double rh[NU];                   // 2 r
   double qf[NX][NX];               // Qh = 2 Q (full; the diagonal case fills the diagonal)
   double rf[NU][NU];               // Rh = 2 R (leg blocks used)
   double W[IPM_NF][9];             // per stance foot-step 3x3 weight of the Newton system
   alignas(16) double P[144];       // P_{k+1}
-  alignas(16) double U[NM][NU]; // iterate (swing entries 0)
+  alignas(16) double U[NM][NU];    // iterate (swing entries 0)
   alignas(16) double dU[NM][NU];
   alignas(16) double rhs[NM][NU];
   alignas(16) double gr[NM][NU];
-  alignas(16) double Y[NM][NU];
-  alignas(16) double By[NM][NU];
   alignas(16) double Us[NM][NU];   // the IPM iterate while a polish overwrites U
-  alignas(16) double X[NM + 1][16];
-  alignas(16) double BU[NM][NU];   // gradient: B_d U_k
-  alignas(16) double nuh[NM][NU];  // gradient: adjoint nu_k (rows 0..11)
-  alignas(16) double la[NM][NU], lb[NM][NU], lc[NM][NU];   // lsolve: per-stage vectors
-  alignas(16) double ph[NM][NU];   // lsolve: p_{k+1}, the backward recursion's input at stage k
-  alignas(16) double dxh[NM][NU];  // lsolve: dx_k
   // per stance foot-step interior-point state in LDS when a lane owns more than one
   // foot-step (NM > 16); with at most 64 foot-steps each lane keeps its one in registers
   std::conditional_t<(IPM_NF > LANES), IpmFootLds<IPM_NF>, IpmFootNone> ft;
 };
+// the Riccati S_k of one robot in its workgroup's global scratch slot
+constexpr int IPM_S_SLOT = kMaxN * 144;   // doubles per slot
 
 // 12 consecutive doubles of a 16-B aligned LDS vector, 16 B per read
 __device__ __forceinline__ void ld12(double (&v)[12], const double* p) {
@@ -125,6 +135,16 @@ __device__ __forceinline__ void st12(double* p, const double (&v)[12]) {
   d2* q = reinterpret_cast<d2*>(p);
 #pragma unroll
   for (int i = 0; i < 6; ++i) q[i] = d2{v[2 * i], v[2 * i + 1]};
+}
+// the same from global memory (the Riccati S_k scratch slot)
+__device__ __forceinline__ void ld12g(double (&v)[12], const double* __restrict__ p) {
+  const d2* q = reinterpret_cast<const d2*>(p);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const d2 x = q[i];
+    v[2 * i] = x[0];
+    v[2 * i + 1] = x[1];
+  }
 }
 __device__ __forceinline__ double dot12(const double (&a)[12], const double (&b)[12]) {
   double s0 = a[0] * b[0], s1 = a[1] * b[1], s2 = a[2] * b[2];
@@ -155,7 +175,7 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 
 // One robot with more than 128 stance variables.  Called by a 64-thread workgroup.
 template <bool FULL, int NM>
-__device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSharedT<NM>& sm,
+__device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSharedT<NM>& sm, double* __restrict__ Sg,
                                                 const float* __restrict__ x0g, const float* __restrict__ xrefg,
                                                 const float* __restrict__ contactg, const float* __restrict__ feetg,
                                                 const float* __restrict__ robotg, float* __restrict__ u0g,
@@ -517,7 +537,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
         double v = 0.0;
         if (r < 12 && lc < 12) {
           v = 0.5 * (sm.TT[lc][r] + sm.TT[r][lc]);
-          sm.S[k][12 * r + lc] = v;
+          Sg[k * 144 + 12 * r + lc] = v;
         }
         Sr[i] = v;
       }
@@ -539,6 +559,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     }
     stage_m(0, Sp, Ep);
     fsync<NT>();   // S_k, M_k for lsolve
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // S_k's global stores, before lsolve reads them
     IPM_T1(1);
   };
 
@@ -580,7 +601,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     for (int e = lane; e < N * NU; e += NT) {
       const int k = e / NU, i = e % NU;
       double sr[12], v[12];
-      ld12(sr, sm.S[k] + 12 * i);
+      ld12g(sr, Sg + k * 144 + 12 * i);
       ld12(v, src[k]);
       dst[k][i] = dot12(sr, v);
     }
@@ -662,7 +683,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       double dxv[12], by[12], sr[12];
       ld12(dxv, sm.dxh[k]);
       ld12(by, sm.By[k]);
-      ld12(sr, sm.S[k] + 12 * i);
+      ld12g(sr, Sg + k * 144 + 12 * i);
 #pragma unroll
       for (int m = 0; m < 12; ++m) {   // A dx on the 12-state
         double a = dxv[m];

@@ -37,7 +37,7 @@ struct Cfg {
   static constexpr int VPL = (NV + LANES - 1) / LANES;   // variables / slots per lane
   static constexpr int VEC = VPL * LANES;     // LDS vector length (entries >= NV are padding)
   static_assert(NW * LANES * 4 * TW == NV * NV, "4 x TW tiles");
-  static_assert(TCN == 4 || TCN == 8 || TCN == 16, "tile rows are reduced over 4, 8 or 16 lanes");
+  static_assert(TCN == 4 || TCN == 8 || TCN == 16 || TCN == 32, "tile rows are reduced over 4 to 32 lanes");
 };
 
 // Every class keeps a copy of H (its register tiles, lane-interleaved) in LDS for
@@ -96,9 +96,25 @@ __device__ __forceinline__ double dpp_shl1(double v) {
   const int hi = __builtin_amdgcn_update_dpp(0, (int)(bits >> 32), DPP_SHL1, 0xF, 0xF, true);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
+// lane i reads lane i + 1 across the whole wave (wave_shl:1): tile rows of 32 lanes span two
+// 16-lane DPP rows, so a foot-step straddling tile columns 15 | 16 needs the wave shift
+constexpr int DPP_WSHL1 = 0x130;
+__device__ __forceinline__ double dpp_wshl1(double v) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)bits, DPP_WSHL1, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(bits >> 32), DPP_WSHL1, 0xF, 0xF, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 
 // Sum 4 row partials over the TCN lanes of a tile row.  Lane keeps row
 // 4tr + 2 bit2(lane) + bit1(lane) (see trow / twriter).
+// lane i <- lane i ^ 16 (ds_swizzle bit mode inside 32 lanes: and 0x1f, xor 0x10)
+__device__ __forceinline__ double swz_xor16(double v) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_swizzle((int)bits, 0x401F);
+  const int hi = __builtin_amdgcn_ds_swizzle((int)(bits >> 32), 0x401F);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 template <int TCN>
 __device__ __forceinline__ double tile_reduce(const double (&acc)[4], int lane) {
   if constexpr (TCN == 4) {   // one-wave class 64 (4 x 16 tiles): lane keeps row 4tr + (lane & 3)
@@ -128,7 +144,8 @@ __device__ __forceinline__ double tile_reduce(const double (&acc)[4], int lane) 
   const double keep = hi2 ? k2[1] : k2[0];
   double y = keep + dpp_d<DPP_XOR2>(send);
   y += dpp_d<DPP_XOR1>(y);
-  if constexpr (TCN == 16) y += dpp_d<DPP_ROR8>(y);
+  if constexpr (TCN >= 16) y += dpp_d<DPP_ROR8>(y);
+  if constexpr (TCN == 32) y += swz_xor16(y);
   return y;
 }
 template <int TCN>
@@ -136,7 +153,9 @@ __device__ __forceinline__ int trow(int tr, int lane) {
   return TCN == 4 ? 4 * tr + (lane & 3) : 4 * tr + 2 * ((lane >> 2) & 1) + ((lane >> 1) & 1);
 }
 template <int TCN>
-__device__ __forceinline__ bool twriter(int lane) { return TCN == 4 ? true : TCN == 16 ? (lane & 9) == 0 : (lane & 1) == 0; }
+__device__ __forceinline__ bool twriter(int lane) {
+  return TCN == 4 ? true : TCN == 32 ? (lane & 25) == 0 : TCN == 16 ? (lane & 9) == 0 : (lane & 1) == 0;
+}
 
 // y = M v, v in LDS; returns row trow<TCN>(tr, lane)'s value
 template <int TCN, int TW>
@@ -783,7 +802,9 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       double zq[4], rq[4];
       if constexpr (TW % 3 == 0) {   // foot-steps start at a register column 3k: never straddle,
         // so the uniform (SGPR) coefficients need no per-lane mask: only tile column tA stores
-        if constexpr (TW == 6) {
+        if constexpr (TW == 3) {   // one foot-step per tile column
+          colcombo_u<0, TW>(W, Rm, e0, e1, e2, rlive, zq, rq);
+        } else if constexpr (TW == 6) {
           if (cA == 0) colcombo_u<0, TW>(W, Rm, e0, e1, e2, rlive, zq, rq);
           else colcombo_u<3, TW>(W, Rm, e0, e1, e2, rlive, zq, rq);
         } else {   // TW = 12
@@ -793,6 +814,13 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
             case 6: colcombo_u<6, TW>(W, Rm, e0, e1, e2, rlive, zq, rq); break;
             default: colcombo_u<9, TW>(W, Rm, e0, e1, e2, rlive, zq, rq); break;
           }
+        }
+      } else if constexpr (TW == 4) {
+        switch (cA) {
+          case 0: colcombo<0, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+          case 1: colcombo<1, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+          case 2: colcombo<2, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
+          default: colcombo<3, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
         }
       } else if constexpr (kAsmCombo) {
         // one computed jump into straight-line cases (mpcqp_combo_asm.h); R's half
@@ -841,8 +869,8 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       if (TW % 3 != 0 && !kAsmCombo && __builtin_expect(cA + 2 >= TW, 0)) {   // straddles tile columns tA, tA + 1
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          zq[r] += dpp_shl1(zq[r]);
-          rq[r] += dpp_shl1(rq[r]);
+          zq[r] += TCN == 32 ? dpp_wshl1(zq[r]) : dpp_shl1(zq[r]);
+          rq[r] += TCN == 32 ? dpp_wshl1(rq[r]) : dpp_shl1(rq[r]);
         }
       }
       if (tc == tA) {
