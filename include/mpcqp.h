@@ -62,8 +62,10 @@ extern "C" {
 
 #define MPCQP_ABI_VERSION 4
 #define MPCQP_ROBOT_STRIDE 16
-#define MPCQP_MAX_HORIZON 20   /* mpcqp_create rejects horizon > 20 (MPCQP_ERR_ARG): the
-                                  per-robot LDS scratch of every class is sized for it */
+#define MPCQP_MAX_HORIZON 32   /* mpcqp_create rejects horizon > 32 (MPCQP_ERR_ARG).  Horizons
+                                  up to 20 use every capacity class; longer ones are solved by
+                                  the interior-point class alone (its per-robot LDS scratch is
+                                  sized for 32 stages, the dense classes' for 20) */
 
 /* error codes (return values) */
 #define MPCQP_OK 0

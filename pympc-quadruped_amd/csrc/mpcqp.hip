@@ -42,8 +42,10 @@ namespace {
 constexpr int NX = 13;      // state dimension (mpc.py:26)
 constexpr int NU = 12;      // input dimension (mpc.py:28)
 constexpr int LANES = 64;
-constexpr int kMaxN = MPCQP_MAX_HORIZON;   // LDS scratch is sized for N <= 20 (include/mpcqp.h)
-static_assert(kMaxN == 20, "the dense classes' and the interior-point class's LDS layouts are sized for N <= 20");
+constexpr int kMaxN = MPCQP_MAX_HORIZON;   // the longest horizon mpcqp_create accepts (include/mpcqp.h)
+constexpr int kDenseN = 20;   // the dense classes' LDS layouts hold N <= 20; longer horizons go to
+                              // the interior-point class, sized for N <= kMaxN
+static_assert(kMaxN >= kDenseN && 4 * kMaxN <= 2 * LANES, "stance lists cover 4 N <= 128 entries");
 #ifndef MPCQP_SPLIT_CHOICE
 #define MPCQP_SPLIT_CHOICE 1   // class 64: wave 1 chooses the next rows, wave 0 reads them; 0: both choose
 #endif
@@ -84,8 +86,7 @@ static_assert(kMaxN == 20, "the dense classes' and the interior-point class's LD
 #define MPCQP_EARLY_CHOICE 1
 #endif
 // staged inputs (floats)
-constexpr int IN_X0 = 0, IN_FEET = 13, IN_ROBOT = 25, IN_CONTACT = 44, IN_XREF = 44 + 4 * kMaxN;
-constexpr int IN_END = IN_XREF + NX * kMaxN;
+constexpr int IN_X0 = 0, IN_FEET = 13, IN_ROBOT = 25, IN_CONTACT = 44;   // + FormT<NM>::IN_XREF
 
 typedef double d2 __attribute__((ext_vector_type(2)));
 typedef double d4 __attribute__((ext_vector_type(4)));   // v_mfma_f64_16x16x4 accumulators (mpcqp_ipm.h)
@@ -708,9 +709,12 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   const int nmax_h = 12 * kp.N;
   const int nmax = ctx->stance_hint > 0 && 3 * ctx->stance_hint < nmax_h ? 3 * ctx->stance_hint : nmax_h;
   const int nmin = 3 * ctx->stance_min;
-  const bool large = nmax > kCap64, huge = nmax > 96, giant = nmax > 128;
+  // horizons beyond the dense classes' LDS layouts (N > kDenseN): the interior-point class
+  // takes the whole batch directly, whatever the stance counts
+  const bool ipm_only = kp.N > kDenseN;
+  const bool large = ipm_only || nmax > kCap64, huge = !ipm_only && nmax > 96, giant = ipm_only || nmax > 128;
   // the first class launched: 0 = class 64, 1 = 96, 2 = 128, 3 = interior point
-  const int first = nmin > 128 ? 3 : nmin > 96 ? 2 : nmin > kCap64 ? 1 : 0;
+  const int first = ipm_only ? 3 : nmin > 128 ? 3 : nmin > 96 ? 2 : nmin > kCap64 ? 1 : 0;
   int* q = nullptr;
   QueueSet* qs = nullptr;
   int cap = 0;
@@ -734,9 +738,11 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   const bool fork = giant && first < 3 && side_stream(qs);
   bool ipm_done = false;
   auto launch_ipm = [&](hipStream_t s) -> hipError_t {
-    // N <= 16 (the reference's default horizon): the 16-stage LDS layout, three robots per CU
-    auto kern = kp.N <= 16 ? (full ? mpcqp_kernel_ipm<true, 16> : mpcqp_kernel_ipm<false, 16>)
-                        : (full ? mpcqp_kernel_ipm<true, kMaxN> : mpcqp_kernel_ipm<false, kMaxN>);
+    // the LDS layout for the horizon: N <= 16 (the reference's default) three robots per CU,
+    // N <= 20 one, longer horizons (up to kMaxN) one
+    auto kern = kp.N <= 16       ? (full ? mpcqp_kernel_ipm<true, 16> : mpcqp_kernel_ipm<false, 16>)
+                : kp.N <= kDenseN ? (full ? mpcqp_kernel_ipm<true, kDenseN> : mpcqp_kernel_ipm<false, kDenseN>)
+                                  : (full ? mpcqp_kernel_ipm<true, kMaxN> : mpcqp_kernel_ipm<false, kMaxN>);
     // persistent workgroups (robots w, w + grid, ...): at most kIpmPerCU per CU, each with a
     // global S_k slot
     const int grid = (int)std::min<long long>(batch, (long long)kIpmPerCU * ctx->ncu);

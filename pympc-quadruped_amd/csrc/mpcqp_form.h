@@ -33,23 +33,27 @@
 // Swing foot-steps are eliminated exactly (their GRFs are 0: ub gives fz <= 0 and
 // the cone gives mu fz >= |fx|, |fy| >= 0), leaving n = 3 * #stance variables.
 
-// Transient formulation scratch (dead once H and g are built)
-struct alignas(16) Form {
+// Transient formulation scratch (dead once H and g are built), sized for horizons N <= NM
+// (the dense classes: kDenseN; the interior-point class: its own stage count)
+template <int NM>
+struct alignas(16) FormT {
+  static constexpr int IN_XREF = IN_CONTACT + 4 * NM, IN_END = IN_XREF + NX * NM;
   float in[IN_END];              // staged inputs (x0, feet, robot record, contact, xref)
   double K[3][NU];               // inv(I_w)[r_leg]x, float32-rounded (B_c rows 6:9)
   double G[3][NU];               // R_z^T K                            (A_c B_c rows 0:3)
-  double E0[kMaxN][16];          // sum_{t >= j} q_s e_t[s]
-  double E1[kMaxN][8];           // sum_{t >= j} t q_s e_t[s]  (s < 6)
+  double E0[NM][16];             // sum_{t >= j} q_s e_t[s]
+  double E1[NM][8];              // sum_{t >= j} t q_s e_t[s]  (s < 6)
   double ii[9];                  // 3x3 work (world inertia, its inverse)
   double rz[2];                  // float32(cos yaw), float32(sin yaw)
   double minv;                   // float32(1/m)
   double q[16];                  // state weights (staged: indexed per lane below)
   // full Q only (KParams::wfull): Q, the raw suffix sums of e_t and t e_t, X0 / X1 and Q X0 / Q X1
   double qf[NX * NX];
-  double es[2][kMaxN][NX];
+  double es[2][NM][NX];
   double X[2][NX][NU];
   double QX[2][NX][NU];
 };
+using Form = FormT<kDenseN>;
 
 // Hessian blocks {Ya, Yb}[c1][c2]: kept for the whole solve (H entries are
 // re-derived from it when a constraint is dropped)
@@ -61,16 +65,18 @@ struct alignas(16) FormY {
   double rf2[NU * NU];
 };
 
-// Per-robot data every class keeps for the solve.
-struct alignas(16) RobotMeta {
+// Per-robot data every class keeps for the solve (horizons N <= NM).
+template <int NM>
+struct alignas(16) RobotMetaT {
   double rows[6][3];             // one-sided cone rows a_r (a_r . f >= b_r)
-  double ub[4 * kMaxN];          // contact * fz_max per stance foot-step (mpc.py:257)
-  int foot_t[4 * kMaxN];         // stance foot-step -> horizon step
-  int foot_leg[4 * kMaxN];       // stance foot-step -> leg
-  int stance_of[4 * kMaxN];      // (step, leg) -> stance foot-step or -1
+  double ub[4 * NM];             // contact * fz_max per stance foot-step (mpc.py:257)
+  int foot_t[4 * NM];            // stance foot-step -> horizon step
+  int foot_leg[4 * NM];          // stance foot-step -> leg
+  int stance_of[4 * NM];         // (step, leg) -> stance foot-step or -1
   int S;
   int fz0_implied;               // mu > 0: the n.f >= 0 row is the half-sum of rows 0 and 1
 };
+using RobotMeta = RobotMetaT<kDenseN>;
 
 template <int NT>
 __device__ __forceinline__ void fsync() {
@@ -90,8 +96,8 @@ __device__ __forceinline__ bool fany(bool v) {
 }
 
 // Stage the robot's inputs in LDS; false if any is non-finite (status NONFINITE).
-template <int NT>
-__device__ __forceinline__ bool form_stage(Form& f, int N, int b, int tid, const float* __restrict__ x0g,
+template <int NT, class F>
+__device__ __forceinline__ bool form_stage(F& f, int N, int b, int tid, const float* __restrict__ x0g,
                                            const float* __restrict__ xrefg, const float* __restrict__ contactg,
                                            const float* __restrict__ feetg, const float* __restrict__ robotg) {
   // The robot's five input slices, staged into LDS with 16-byte loads: each slice is
@@ -118,7 +124,7 @@ __device__ __forceinline__ bool form_stage(Form& f, int N, int b, int tid, const
     const float* const q = i == 0 ? p0 : i == 1 ? p1 : i == 2 ? p2 : i == 3 ? p3 : p4;
     const int cb = i == 0 ? 0 : i == 1 ? c1 : i == 2 ? c2 : i == 3 ? c3 : c4;
     const int len = i == 0 ? NX : i == 1 ? 12 : i == 2 ? 12 : i == 3 ? 4 * N : NX * N;   // robot: 12 fields read
-    const int dst = i == 0 ? IN_X0 : i == 1 ? IN_FEET : i == 2 ? IN_ROBOT : i == 3 ? IN_CONTACT : IN_XREF;
+    const int dst = i == 0 ? IN_X0 : i == 1 ? IN_FEET : i == 2 ? IN_ROBOT : i == 3 ? IN_CONTACT : F::IN_XREF;
     const uintptr_t base = ((uintptr_t)q & ~(uintptr_t)15) + 16 * (uintptr_t)(c - cb);
     const float4 v = *reinterpret_cast<const float4*>(base);
     const int e = (int)(((intptr_t)base - (intptr_t)q) >> 2);   // slice index of v.x (may be < 0)
@@ -137,7 +143,8 @@ __device__ __forceinline__ bool form_stage(Form& f, int N, int b, int tid, const
 
 // Stance list from the gait table (one wave: lanes cover 4N <= 128 entries).
 // Returns S (wave-uniform).  Writes meta.{foot_t, foot_leg, ub, stance_of, S}.
-__device__ __forceinline__ int form_stance(const Form& f, RobotMeta& mt, int N, int lane) {
+template <class F, class MT>
+__device__ __forceinline__ int form_stance(const F& f, MT& mt, int N, int lane) {
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const int nk = 4 * N;
   const float c0 = lane < nk ? f.in[IN_CONTACT + lane] : 0.f;
@@ -165,7 +172,8 @@ __device__ __forceinline__ int form_stance(const Form& f, RobotMeta& mt, int N, 
 }
 
 // e_t's state component sc at horizon step t (0-based: e_t = A^{t+1} x0 - xref_t)
-__device__ __forceinline__ double form_e(const Form& f, int sc, int t, double h) {
+template <class F>
+__device__ __forceinline__ double form_e(const F& f, int sc, int t, double h) {
   const float* xin = f.in + IN_X0;
   auto rz = [&](int a, int bb) -> double {
     return a == 2 ? (bb == 2 ? 1.0 : 0.0) : (bb == 2 ? 0.0 : (a == bb ? f.rz[0] : (a == 0 ? -f.rz[1] : f.rz[1])));
@@ -177,14 +185,14 @@ __device__ __forceinline__ double form_e(const Form& f, int sc, int t, double h)
   else if (sc == 11) n1 = h * g12;
   if (sc == 5) n2 = h * h * g12;
   const double k = (double)(t + 1);
-  return x0s + k * n1 + 0.5 * k * (k - 1.0) * n2 - (double)f.in[IN_XREF + t * NX + sc];
+  return x0s + k * n1 + 0.5 * k * (k - 1.0) * n2 - (double)f.in[F::IN_XREF + t * NX + sc];
 }
 
 // Full (non-diagonal) Q / R (KParams::wfull): E0 / E1 = Q times the suffix sums of e_t and
 // t e_t, and the closed-form blocks Y00 = X0^T Q X0, Y01 = X0^T Q X1, Y11 = X1^T Q X1 with X0
 // = B_d, X1 = Nm B_d written out (K, G, minv are in LDS: called after their barrier).
-template <int NT>
-__device__ __forceinline__ void form_model_full(const KParams& P, Form& f, FormY& fy, int N, int tid) {
+template <int NT, class F>
+__device__ __forceinline__ void form_model_full(const KParams& P, F& f, FormY& fy, int N, int tid) {
   const double h = P.dt;
   fsync<NT>();   // K, G (written just before by threads < 36) are read below
   for (int e = tid; e < NX * NX; e += NT) f.qf[e] = P.wfull[e];
@@ -250,8 +258,8 @@ __device__ __forceinline__ void form_model_full(const KParams& P, Form& f, FormY
 }
 
 // Model (float32-faithful), cone rows, Ya/Yb, horizon suffix sums.  All NT threads.
-template <int NT>
-__device__ __forceinline__ void form_model(const KParams& P, Form& f, FormY& fy, RobotMeta& mt, int N, int tid) {
+template <int NT, class F, class MT>
+__device__ __forceinline__ void form_model(const KParams& P, F& f, FormY& fy, MT& mt, int N, int tid) {
   const float* const rbs = f.in + IN_ROBOT;
   const double h = P.dt;
   // ---- R_z, I_w = float32(float32(R_z I_B) R_z^T), inverse (mpc.py:178-182)
@@ -353,7 +361,7 @@ __device__ __forceinline__ void form_model(const KParams& P, Form& f, FormY& fy,
     double e0 = 0.0, e1 = 0.0;
     for (int t = N - 1; t >= 0; --t) {
       const double k = (double)(t + 1);
-      const double e = x0s + k * n1 + 0.5 * k * (k - 1.0) * n2 - (double)f.in[IN_XREF + t * NX + sc];
+      const double e = x0s + k * n1 + 0.5 * k * (k - 1.0) * n2 - (double)f.in[F::IN_XREF + t * NX + sc];
       e0 = fma(q, e, e0);
       e1 = fma((double)t * q, e, e1);
       f.E0[t][sc] = e0;
@@ -383,7 +391,8 @@ __device__ __forceinline__ void form_model(const KParams& P, Form& f, FormY& fy,
 }
 
 // g[a] for the stance variable a < n held by this thread (mpc.py:233)
-__device__ __forceinline__ double form_g(const KParams& P, const Form& f, const RobotMeta& mt, int a) {
+template <class F, class MT>
+__device__ __forceinline__ double form_g(const KParams& P, const F& f, const MT& mt, int a) {
   const double h = P.dt;
   const int sf = a / 3, ax = a % 3;
   const int j = mt.foot_t[sf], cc = 3 * mt.foot_leg[sf] + ax;

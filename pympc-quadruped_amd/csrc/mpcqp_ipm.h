@@ -75,7 +75,7 @@ struct alignas(16) IpmSharedT {
   static constexpr int IPM_NF = 4 * NM;
   union {
     struct {
-      Form f;
+      FormT<NM> f;
       FormY fy;
     } fa;                          // formulation scratch (dead once Bm / x0 / xr are copied)
     struct {
@@ -96,7 +96,7 @@ struct alignas(16) IpmSharedT {
       };
     };
   };
-  RobotMeta mt;
+  RobotMetaT<NM> mt;
   alignas(16) double Bm[12][12];   // B_d rows 0..11 (row 12 is 0)
   alignas(16) double BmT[12][12];  // its transpose
   alignas(16) double TT[12][12];   // factor scratch: (I + P E)^T, then S_k^T
@@ -187,7 +187,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
   const double h = KP.dt;
 
   // ------------------------------------------------ formulation (mpcqp_form.h)
-  Form& smf = sm.fa.f;
+  auto& smf = sm.fa.f;
   if (!form_stage<NT>(smf, N, b, lane, x0g, xrefg, contactg, feetg, robotg)) {
     write_empty_t<NT>(b, lane, N, MPCQP_STATUS_NONFINITE, u0g, Ug, statusg, itersg);
     return;
@@ -237,7 +237,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       for (int e = lane; e < NX * NX; e += NT) sm.qf[e / NX][e % NX] = 2.0 * KP.wfull[e];
       for (int e = lane; e < NU * NU; e += NT) sm.rf[e / NU][e % NU] = 2.0 * KP.wfull[NX * NX + e];
     }
-    for (int e = lane; e < N * NX; e += NT) sm.xr[e / NX][e % NX] = (double)smf.in[IN_XREF + e];
+    for (int e = lane; e < N * NX; e += NT) sm.xr[e / NX][e % NX] = (double)smf.in[FormT<NM>::IN_XREF + e];
     for (int e = lane; e < N * NU; e += NT) sm.U[e / NU][e % NU] = 0.0;
   }
   fsync<NT>();   // the formulation scratch (union with S) is dead from here on

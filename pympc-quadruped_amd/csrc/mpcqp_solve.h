@@ -48,7 +48,7 @@ template <int NV>
 struct FormArea {
   Form f;
   FormY fy;
-  d2 mt_tab[kMaxN * kMaxN];   // (Ta, m) of every foot-step step pair (ja, jb) for the diagonal-Q H build
+  d2 mt_tab[kDenseN * kDenseN];   // (Ta, m) of every foot-step step pair (ja, jb) for the diagonal-Q H build
 };
 template <int NV>
 struct alignas(16) SharedT {

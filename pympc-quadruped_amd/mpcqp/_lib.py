@@ -22,7 +22,7 @@ STATUS_TOO_LARGE = 3
 STATUS_NONFINITE = 4
 STATUS_UNSUPPORTED = 5
 ROBOT_STRIDE = 16
-MAX_HORIZON = 20    # MPCQP_MAX_HORIZON: mpcqp_create rejects a longer horizon
+MAX_HORIZON = 32    # MPCQP_MAX_HORIZON: mpcqp_create rejects a longer horizon
 
 # every symbol declared in include/mpcqp.h
 EXPORTED_SYMBOLS = (

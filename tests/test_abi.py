@@ -80,7 +80,7 @@ def test_horizon_limit_is_the_create_limit():
     from mpcqp import _lib, LinearMpc
     src = open(HEADER).read()
     limit = int(re.search(r"#define MPCQP_MAX_HORIZON (\d+)", src).group(1))
-    assert limit == _lib.MAX_HORIZON == 20
+    assert limit == _lib.MAX_HORIZON == 32
     lib = _lib.load()
     ctx = ctypes.c_void_p()
     p = _lib.default_params(limit + 1)
@@ -90,7 +90,7 @@ def test_horizon_limit_is_the_create_limit():
     assert rc != -1   # accepted (no GPU here: MPCQP_ERR_HIP from the device query)
     if rc == 0:
         lib.mpcqp_destroy(ctx)
-    with pytest.raises(ValueError, match="1..20"):
+    with pytest.raises(ValueError, match="1..32"):
         LinearMpc(horizon=limit + 1, device="cuda:0")
 
 

@@ -332,6 +332,34 @@ def test_random_contact_patterns_every_class(N):
     assert bt["robot"][:, R_NX:R_NZ + 1].shape == (B, 3)
 
 
+@pytest.mark.parametrize("N", [24, 32])
+def test_long_horizons_interior_point(N):
+    """Horizons beyond the dense classes' 20-stage layouts (LinearMpcConfig.horizon is a
+    free value, linear_mpc_configs.py:11; MPCQP_MAX_HORIZON = 32): the interior-point class
+    takes the whole batch -- gait-table trot / pace / bound schedules, a standing and a
+    sparse robot (n well below 128) and a flight schedule -- each robot's u0 and U against
+    the float64 oracle at the contract and the interior-point precision guard."""
+    from mpcqp.synthetic import make_batch
+    B = 10 if N == 32 else 12
+    rng = np.random.default_rng(300 + N)
+    bt = make_batch(B, N, seed=400 + N, gaits=("trot10", "pace10", "bound8"), robots=("a1", "aliengo"),
+                    tilt_deg=10.0)
+    bt["contact"][0] = 1.0                                              # standing: n = 12 N
+    bt["contact"][1] = (rng.random((N, 4)) < 0.2).astype(np.float32)    # sparse: n < 128
+    bt["contact"][2] = 0.0                                              # flight: n = 0
+    u0, U, status, iters = _solve(_engine(N), bt)
+    assert (status == 0).all(), status
+    worst = 0.0
+    for b in range(B):
+        x, _, _ = oracle_solution(bt, b, N)
+        e = max(rel_err_u0(u0[b], x[:12]), rel_err_u0(U[b], x))
+        assert e < TOL_U0, (b, e)
+        worst = max(worst, e)
+    assert worst < TOL_ACHIEVED_IPM, worst
+    assert np.all(U[2] == 0) and np.all(u0[2] == 0)
+    assert iters[0] > 0   # Newton factorisations: the interior-point class solved it
+
+
 def test_stance_range_direct_classes():
     """mpcqp_set_stance_range: when the range rules out the smaller classes, the first
     possible class takes the batch directly -- the same kernels and arithmetic as the
