@@ -64,6 +64,7 @@ def solve_qp_dual_active_set(H, g, C, lb, ub, max_iter=10000, tol=1e-11):
             break
         npv = A[p]
         u_p = 0.0
+        done = False
         while True:
             it += 1
             if it > max_iter:
@@ -88,6 +89,15 @@ def solve_qp_dual_active_set(H, g, C, lb, ub, max_iter=10000, tol=1e-11):
                 t2 = np.inf
             t = min(t1, t2)
             if not np.isfinite(t):
+                # p is dependent on the active set and no multiplier can move.  In exact
+                # arithmetic that is infeasibility, which the MPC QP cannot have (U = 0 is
+                # feasible); a violation at rounding level (a flight schedule's forced-zero
+                # GRFs at N = 32: s = -3e-11 against dn = 4e4) is rounding noise of the
+                # J / R updates, and p is the most violated row, so every row is satisfied
+                # to that level.
+                if s[p] >= -1e-8 * scale:
+                    done = True
+                    break
                 raise RuntimeError("QP infeasible (cannot happen for the MPC QP)")
             if not np.isfinite(t2):
                 # pure dual step: constraint p is dependent on the active set
@@ -105,6 +115,8 @@ def solve_qp_dual_active_set(H, g, C, lb, ub, max_iter=10000, tol=1e-11):
                 u = np.append(u, u_p)
                 break
             R, J, active, u = _drop(R, J, active, u, l_drop)
+        if done:
+            break
     y = np.zeros(np.asarray(C).shape[0])
     for k, j in enumerate(active):
         y[src[j]] += sgn[j] * u[k]

@@ -357,7 +357,7 @@ __device__ __forceinline__ int xcd_robot(int bid, int B) {
 
 // class 64's capacity (stance variables)
 constexpr int kCap64 = 64;
-// interior-point class: persistent workgroups per CU (three robots fit a CU's LDS at N <= 16)
+// interior-point class: global S_k slots per CU (at most three robots fit a CU's LDS)
 constexpr int kIpmPerCU = 4;
 
 // Class NV = 64: one 2-wave workgroup per robot of the batch.  Robots with more
@@ -443,38 +443,54 @@ __global__ __launch_bounds__(Cfg<128>::NT) MPCQP_C128_ATTR void mpcqp_kernel_128
   }
 }
 
-// Large class (n > 128: standing schedules at N >= 11): one wave per queued robot,
-// Riccati-factored interior point + active-set polish (mpcqp_ipm.h).  Same launch /
-// reset protocol as class 128.  FULL: non-diagonal weights (mpcqp_set_weights).
+// Riccati-factored interior point + active-set polish (mpcqp_ipm.h).  Same launch / reset
+// protocol as class 128.  FULL: non-diagonal weights (mpcqp_set_weights).
+// A free slot of the interior-point class's global S_k scratch: one bit per slot in `bits`
+// (nw words), claimed with atomicOr, released with atomicAnd.  More slots than robots can
+// be resident at once (LDS-bound: <= 3 per CU; kIpmPerCU = 4 slots per CU), so the search
+// always finds one.  Called by one lane.
+__device__ __forceinline__ int ipm_claim_slot(unsigned* bits, int nw, int start) {
+  for (int i = 0;; ++i) {
+    const int w = (start + i) % nw;
+    unsigned m = ~__hip_atomic_load(&bits[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (m) {
+      const int bit = __builtin_ctz(m);
+      const unsigned old = atomicOr(&bits[w], 1u << bit);
+      if (!(old & (1u << bit))) return 32 * w + bit;
+      m &= ~old & ~(1u << bit);
+    }
+  }
+}
+
+// Large class (n > 128, and every robot at N > 20): one wave per robot; its Riccati S_k in
+// a global slot claimed for the robot's solve (sbits: slot bitmap, nsw words)
 template <bool FULL, int NM>
 __global__ __launch_bounds__(LANES) void mpcqp_kernel_ipm(
     KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
-    int* __restrict__ queue, int direct_B, double* __restrict__ sscratch) {
+    int* __restrict__ queue, int direct_B, double* __restrict__ sscratch, unsigned* __restrict__ sbits,
+    int nsw) {
   __shared__ IpmSharedT<NM> sm;
   const int tid = threadIdx.x;
-  // persistent workgroups (its global S_k slot is the workgroup's) taking robots by ticket
-  // (queue[1]): a workgroup that finishes early takes the next robot, whatever the residency.
-  // The last workgroup to run out of tickets (queue[3] counts them) resets the queue header
-  // for the next launch -- only then can no workgroup still take a ticket.
-  double* const Sg = sscratch + (size_t)blockIdx.x * IPM_S_SLOT;
-  // direct_B > 0: the caller's stance range rules the dense classes out, ticket = robot
+  const int k = blockIdx.x;
+  // direct_B > 0: the caller's stance range (or N > 20) rules the dense classes out, robot = k
   const bool direct = direct_B > 0;
   const int cnt = direct ? direct_B : uni(__hip_atomic_load(&queue[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  if (cnt == 0) return;   // nothing queued: no counter is touched, none needs a reset
-  while (true) {
-    int t = 0;
-    if (tid == 0) t = atomicAdd(&queue[1], 1);
-    t = __builtin_amdgcn_readlane(t, 0);
-    if (t >= cnt) break;
-    const int b = direct ? t : uni(queue[4 + t]);
-    solve_robot_ipm<FULL, NM>(P, b, sm, Sg, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg);
-  }
-  if (tid == 0 && atomicAdd(&queue[3], 1) == (int)gridDim.x - 1) {
-    atomicExch(&queue[0], 0);
-    atomicExch(&queue[1], 0);
-    atomicExch(&queue[3], 0);
+  if (k >= cnt) return;   // idle workgroups touch no counter
+  const int b = direct ? k : uni(queue[4 + k]);
+  int slot = 0;
+  if (tid == 0) slot = ipm_claim_slot(sbits, nsw, k % nsw);
+  slot = __builtin_amdgcn_readlane(slot, 0);
+  solve_robot_ipm<FULL, NM>(P, b, sm, sscratch + (size_t)slot * IPM_S_SLOT, x0g, xrefg, contactg, feetg, robotg, u0g,
+                            Ug, statusg, itersg);
+  if (tid == 0) {
+    atomicAnd(&sbits[slot >> 5], ~(1u << (slot & 31)));   // the solve's S_k reads are done
+    // only the queued robots count themselves; the last one resets the queue
+    if (!direct && atomicAdd(&queue[2], 1) == cnt - 1) {
+      atomicExch(&queue[0], 0);
+      atomicExch(&queue[2], 0);
+    }
   }
 }
 
@@ -725,10 +741,17 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
     q = qs->buf;
   }
   if (giant && !qs->sscratch) {   // the interior-point class's global S_k slots (first use)
-    const int slots = kIpmPerCU * ctx->ncu;
-    if (hipMalloc(&qs->sscratch, sizeof(double) * IPM_S_SLOT * (size_t)slots) != hipSuccess) {
+    const int slots = 32 * ((kIpmPerCU * ctx->ncu + 31) / 32);
+    const size_t sbytes = sizeof(double) * IPM_S_SLOT * (size_t)slots;
+    if (hipMalloc(&qs->sscratch, sbytes + slots / 8) != hipSuccess) {
       qs->sscratch = nullptr;
       return set_err(ctx, MPCQP_ERR_ALLOC, "interior-point scratch allocation failed");
+    }
+    // the slot bitmap after the slots: all free (every solve releases its slot)
+    if (hipMemsetAsync((char*)qs->sscratch + sbytes, 0, slots / 8, st) != hipSuccess) {
+      (void)hipFree(qs->sscratch);
+      qs->sscratch = nullptr;
+      return set_err(ctx, MPCQP_ERR_HIP, "interior-point scratch init failed");
     }
     qs->sslots = slots;
   }
@@ -743,12 +766,11 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
     auto kern = kp.N <= 16       ? (full ? mpcqp_kernel_ipm<true, 16> : mpcqp_kernel_ipm<false, 16>)
                 : kp.N <= kDenseN ? (full ? mpcqp_kernel_ipm<true, kDenseN> : mpcqp_kernel_ipm<false, kDenseN>)
                                   : (full ? mpcqp_kernel_ipm<true, kMaxN> : mpcqp_kernel_ipm<false, kMaxN>);
-    // persistent workgroups (robots w, w + grid, ...): at most kIpmPerCU per CU, each with a
-    // global S_k slot
-    const int grid = (int)std::min<long long>(batch, (long long)kIpmPerCU * ctx->ncu);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(LANES), 0, s, kp, x0, xref, contact, feet, robot, u0, U,
+    // one workgroup per robot of the batch (the queued ones beyond the count exit at once)
+    unsigned* sbits = (unsigned*)(qs->sscratch + (size_t)IPM_S_SLOT * qs->sslots);
+    hipLaunchKernelGGL(kern, dim3(batch), dim3(LANES), 0, s, kp, x0, xref, contact, feet, robot, u0, U,
                        (int*)status, (int*)iters, q + 2 * (4 + (size_t)cap), first == 3 ? (int)batch : 0,
-                       qs->sscratch);
+                       qs->sscratch, sbits, qs->sslots / 32);
     ipm_done = true;
     return hipGetLastError();
   };
