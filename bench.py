@@ -317,26 +317,37 @@ def bench_config1(args):
         fz_max = al["fz_max"]
 
     N = LinearMpcConfig.horizon
-    ctl = mpc.ModelPredictiveController(LinearMpcConfig, AliengoConfig)
     n_iter = (args.warmup + args.steps) * LinearMpcConfig.iteration_between_mpc
-    mpc_ms, other_ms, states = [], [], []
     v_des = np.array([1.2, 0.0, 0.0])
-    for it in range(n_iter):
-        rd = _SyntheticRobotData(it * 1e-3)
-        table = gait_table(args.gait, (it // 20) % 10, N).reshape(-1)
-        t0 = time.perf_counter()
-        ctl.update_robot_state(rd)
-        u = ctl.update_mpc_if_needed(it, v_des, 0.0, table, solver="drake")
-        dt = (time.perf_counter() - t0) * 1e3
-        if it >= args.warmup * 20:
-            if it % 20 == 0:
-                mpc_ms.append(dt)
-                if len(states) < 64:
-                    states.append((ctl.current_state.copy(), ctl.ref_traj.copy(), table.copy(),
-                                   [np.asarray(f) for f in rd.pos_base_feet]))
-            else:
-                other_ms.append(dt)
-    assert np.all(np.isfinite(u))
+
+    def run(warm):
+        """The control loop; `warm` False: the engine's warm start (the previous tick's
+        active set, interior-point class only) disabled, every tick solved cold."""
+        ctl = mpc.ModelPredictiveController(LinearMpcConfig, AliengoConfig)
+        mpc_ms, other_ms, states, iters = [], [], [], []
+        for it in range(n_iter):
+            rd = _SyntheticRobotData(it * 1e-3)
+            table = gait_table(args.gait, (it // 20) % 10, N).reshape(-1)
+            if it == 0 and not warm:
+                ctl._get_engine().set_warm_start(0)
+            t0 = time.perf_counter()
+            ctl.update_robot_state(rd)
+            u = ctl.update_mpc_if_needed(it, v_des, 0.0, table, solver="drake")
+            dt = (time.perf_counter() - t0) * 1e3
+            if it >= args.warmup * 20:
+                if it % 20 == 0:
+                    mpc_ms.append(dt)
+                    iters.append(int(ctl._dev["iters"].item()))
+                    if len(states) < 64:
+                        states.append((ctl.current_state.copy(), ctl.ref_traj.copy(), table.copy(),
+                                       [np.asarray(f) for f in rd.pos_base_feet]))
+                else:
+                    other_ms.append(dt)
+        assert np.all(np.isfinite(u))
+        return mpc_ms, other_ms, states, iters
+
+    mpc_ms, other_ms, states, iters = run(True)
+    cold_ms, _, _, cold_iters = run(False)
     cpu = None
     if not args.no_cpu:
         from mpcqp.params import pack_robot, ROBOT_PRESETS
@@ -360,6 +371,12 @@ def bench_config1(args):
                                f"LinearMpcConfig.horizon = 16, gait {args.gait}", "batch": 1, "horizon": N,
                    "gait": args.gait},
         "mpc_tick_ms": {"median": med, "p90": float(np.percentile(mpc_ms, 90)), "mean": float(np.mean(mpc_ms))},
+        "warm_start": "the drop-in's default: each tick's interior-point solve (n > 128) starts from the "
+                      "previous tick's verified active set (mpcqp_set_warm_start); the dense classes "
+                      "always start cold",
+        "iterations_median": float(np.median(iters)),
+        "cold_mpc_tick_ms": {"median": float(np.median(cold_ms)), "p90": float(np.percentile(cold_ms, 90)),
+                             "iterations_median": float(np.median(cold_iters))},
         "other_tick_ms": {"median": float(np.median(other_ms)), "p90": float(np.percentile(other_ms, 90))},
         "cpu_baseline": cpu,
     }))

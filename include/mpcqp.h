@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define MPCQP_ABI_VERSION 4
+#define MPCQP_ABI_VERSION 5
 #define MPCQP_ROBOT_STRIDE 16
 #define MPCQP_MAX_HORIZON 32   /* mpcqp_create rejects horizon > 32 (MPCQP_ERR_ARG).  Horizons
                                   up to 20 use every capacity class; longer ones are solved by
@@ -135,6 +135,24 @@ int mpcqp_set_stance_hint(mpcqp_ctx* ctx, int32_t max_stance);
  * MPCQP_ERR_ARG when min_stance > 4 * horizon (no schedule has that many) or
  * min_stance > max_stance > 0. */
 int mpcqp_set_stance_range(mpcqp_ctx* ctx, int32_t min_stance, int32_t max_stance);
+
+/* Warm start (ABI 5; no counterpart in the reference, whose Drake solve starts cold every
+ * MPC tick, mpc.py:277-286): per-robot memory of the last verified active set, for
+ * callers that solve the same robots tick after tick (the drop-in controller, a fleet in
+ * a simulation loop).  The interior-point class (robots with more than 128 stance
+ * variables, e.g. Gait.STANDING at N >= 11) then first tries the remembered rows -- one
+ * equality-constrained solve and the KKT check its polish always runs, corrected up to 8
+ * times -- and runs the interior point only when that fails.  The result does not depend
+ * on the memory: a status-OK solution is the checked optimum either way.
+ *   memory    DEVICE buffer of capacity * MPCQP_WARM_BYTES bytes, zero-filled by the
+ *             caller before first use (zero = nothing remembered).  Robot b of every later
+ *             mpcqp_solve on this context reads and rewrites memory + b * MPCQP_WARM_BYTES
+ *             (byte 4 k + leg: 0x80 | the foot-step's active cone rows; b >= capacity: no
+ *             memory).  Solves running concurrently on different streams must not share it.
+ *   NULL / capacity 0 disables (the default).  The dense classes (n <= 128) do not use it.
+ * MPCQP_ERR_ARG for capacity < 0, or memory NULL with capacity > 0. */
+#define MPCQP_WARM_BYTES 128   /* 4 * MPCQP_MAX_HORIZON */
+int mpcqp_set_warm_start(mpcqp_ctx* ctx, void* memory, int32_t capacity);
 
 /* ---- the hot path's callers on the device -------------
  *

@@ -46,6 +46,7 @@ constexpr int kMaxN = MPCQP_MAX_HORIZON;   // the longest horizon mpcqp_create a
 constexpr int kDenseN = 20;   // the dense classes' LDS layouts hold N <= 20; longer horizons go to
                               // the interior-point class, sized for N <= kMaxN
 static_assert(kMaxN >= kDenseN && 4 * kMaxN <= 2 * LANES, "stance lists cover 4 N <= 128 entries");
+static_assert(MPCQP_WARM_BYTES == 4 * kMaxN, "warm-start memory: one byte per (stage, leg)");
 #ifndef MPCQP_SPLIT_CHOICE
 #define MPCQP_SPLIT_CHOICE 1   // class 64: wave 1 chooses the next rows, wave 0 reads them; 0: both choose
 #endif
@@ -98,6 +99,8 @@ struct KParams {
   double q[NX];
   double r[NU];
   const double* wfull;   // device: full Q (13 x 13) then R (12 x 12), row-major; nullptr = diagonal q, r
+  unsigned char* warm;   // device: per-robot warm-start memory (mpcqp_set_warm_start), or nullptr
+  int warm_cap;          // robots with memory
 };
 
 // Diagnostic build only (-DMPCQP_STAMPS): per-phase s_memtime stamps and per-section
@@ -539,6 +542,8 @@ struct mpcqp_ctx {
   double* wdev;       // full Q (13 x 13) then R (12 x 12) on the device (mpcqp_set_weights); nullptr: diagonal
   double q_full[13 * 13];   // the current weights as whole matrices (host copies: a NULL argument
   double r_full[12 * 12];   // of mpcqp_set_weights keeps that matrix, off-diagonal entries included)
+  unsigned char* warm;   // warm-start memory (caller-owned device buffer), mpcqp_set_warm_start
+  int warm_cap;
   double dt_control;  // planner constants (mpcqp_set_planner)
   double gravity;
   double max_pos_error;
@@ -668,6 +673,8 @@ int mpcqp_create(const mpcqp_params* p, int32_t device, mpcqp_ctx** out) {
   ctx->ncu = 0;
   ctx->use_clock = 0;
   ctx->wdev = nullptr;
+  ctx->warm = nullptr;
+  ctx->warm_cap = 0;
   for (int i = 0; i < 13 * 13; ++i) ctx->q_full[i] = (i % 14 == 0) ? p->q_diag[i / 14] : 0.0;
   for (int i = 0; i < 12 * 12; ++i) ctx->r_full[i] = (i % 13 == 0) ? p->r_diag[i / 13] : 0.0;
   ctx->dt_control = 0.001;    // linear_mpc_configs.py:6
@@ -677,6 +684,15 @@ int mpcqp_create(const mpcqp_params* p, int32_t device, mpcqp_ctx** out) {
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->ncu = prop.multiProcessorCount;
   if (ctx->ncu <= 0) ctx->ncu = 256;
   *out = ctx;
+  return MPCQP_OK;
+}
+
+int mpcqp_set_warm_start(mpcqp_ctx* ctx, void* memory, int32_t capacity) {
+  if (!ctx) return MPCQP_ERR_ARG;
+  if (capacity < 0 || (capacity > 0 && !memory))
+    return set_err(ctx, MPCQP_ERR_ARG, "warm start: capacity < 0, or no memory for capacity > 0");
+  ctx->warm = capacity > 0 ? static_cast<unsigned char*>(memory) : nullptr;
+  ctx->warm_cap = capacity > 0 ? capacity : 0;
   return MPCQP_OK;
 }
 
@@ -714,6 +730,8 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   for (int i = 0; i < NX; ++i) kp.q[i] = ctx->params.q_diag[i];
   for (int i = 0; i < NU; ++i) kp.r[i] = ctx->params.r_diag[i];
   kp.wfull = ctx->wdev;
+  kp.warm = ctx->warm;
+  kp.warm_cap = ctx->warm_cap;
   const bool full = ctx->wdev != nullptr;   // the dense classes' full-weight instantiations
   hipStream_t st = (hipStream_t)stream;
   // A robot has n = 3 * #stance <= 12 N variables.  Robots with more than 64 are queued

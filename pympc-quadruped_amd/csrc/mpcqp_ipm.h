@@ -729,37 +729,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
   const double hscale = 1.0 + sgpr_d(wave_max_d(hmax));
   const double tol_g = 1e-9 * gscale, tol_h = 1e-9 * hscale;
 
-  // ---- start: minimiser under a mild barrier weight, slacks shifted into the interior
-  for (int j = lane; j < S; j += NT) {
-    double d[6], rh[kRh], wv[9];
-#pragma unroll
-    for (int r = 0; r < 6; ++r) d[r] = 1e-2;
-    legrh(j, rh);
-    ipm_foot_weight(rw, liv, d, rh, wv);
-#pragma unroll
-    for (int e = 0; e < 9; ++e) sm.W[j][e] = wv[e];
-  }
-  for (int e = lane; e < N * NU; e += NT) sm.rhs[e / NU][e % NU] = -sm.gr[e / NU][e % NU];
-  fsync<NT>();
-  factor();
-  ++nfact;
-  lsolve();
-  for (int e = lane; e < N * NU; e += NT) sm.U[e / NU][e % NU] = sm.dU[e / NU][e % NU];
-  fsync<NT>();
-  for (int j = lane; j < S; j += NT) {
-    double f[3];
-    foot(j, sm.U, f);
-    const double h5 = -sm.mt.ub[j];
-#pragma unroll
-    for (int r = 0; r < 6; ++r) {
-      const bool on = (liv >> r) & 1;
-      FS(j)[r] = on ? fmax(adot(r, f) - (r == 5 ? h5 : 0.0), 1.0) : 1.0;
-      FL(j)[r] = on ? 1.0 : 0.0;
-    }
-  }
-  fsync<NT>();
-
-  // ---- active-set polish on the rows sm.fact; true when verified (sm.U = the optimum)
+  // ---- active-set polish on the rows FACT; true when verified (sm.U = the optimum)
   auto polish = [&]() -> bool {
     for (int j = lane; j < S; j += NT) {
       double rh[kRh], pj[9], fp[3], wv[9];
@@ -843,10 +813,77 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
 #endif
     return stat < IPM_STAT_TOL * gscale && smin > -tol_h && lminw > -tol_g;
   };
+  // polish, then correct the set (violated rows in, the most negative multiplier out)
+  // until it verifies, stops changing or IPM_NCORR corrections are spent
+  auto polish_corrected = [&]() -> bool {
+    for (int corr = 0; corr <= IPM_NCORR; ++corr) {
+      int changed = 0;
+      for (int j = lane; j < S; j += NT) FPREV(j) = FACT(j);
+      fsync<NT>();
+      if (polish()) return true;
+      for (int j = lane; j < S; j += NT) changed |= FACT(j) != FPREV(j);
+      if (!__any(changed)) break;
+    }
+    return false;
+  };
+
+  bool done = false;
+  // ---- warm start (mpcqp_set_warm_start): the rows this robot's last verified solve had
+  // active at the same (stage, leg); the cold start below when they do not verify
+  unsigned char* const wmem = KP.warm && b < KP.warm_cap ? KP.warm + (size_t)b * MPCQP_WARM_BYTES : nullptr;
+  if (wmem) {
+    int known = 0;
+    for (int j = lane; j < S; j += NT) {
+      const int v = wmem[4 * sm.mt.foot_t[j] + sm.mt.foot_leg[j]];
+      FACT(j) = v & liv;
+      known |= v & 0x80;
+    }
+    if (__any(known)) {
+      if (polish_corrected()) {
+        done = true;
+        status = MPCQP_STATUS_OK;
+      } else {   // back to U = 0 and its gradient for the cold start
+        for (int e = lane; e < N * NU; e += NT) sm.U[e / NU][e % NU] = 0.0;
+        fsync<NT>();
+        gradient();
+      }
+    }
+  }
+
+  // ---- start: minimiser under a mild barrier weight, slacks shifted into the interior
+  if (!done) {
+    for (int j = lane; j < S; j += NT) {
+      double d[6], rh[kRh], wv[9];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) d[r] = 1e-2;
+      legrh(j, rh);
+      ipm_foot_weight(rw, liv, d, rh, wv);
+#pragma unroll
+      for (int e = 0; e < 9; ++e) sm.W[j][e] = wv[e];
+    }
+    for (int e = lane; e < N * NU; e += NT) sm.rhs[e / NU][e % NU] = -sm.gr[e / NU][e % NU];
+    fsync<NT>();
+    factor();
+    ++nfact;
+    lsolve();
+    for (int e = lane; e < N * NU; e += NT) sm.U[e / NU][e % NU] = sm.dU[e / NU][e % NU];
+    fsync<NT>();
+    for (int j = lane; j < S; j += NT) {
+      double f[3];
+      foot(j, sm.U, f);
+      const double h5 = -sm.mt.ub[j];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        const bool on = (liv >> r) & 1;
+        FS(j)[r] = on ? fmax(adot(r, f) - (r == 5 ? h5 : 0.0), 1.0) : 1.0;
+        FL(j)[r] = on ? 1.0 : 0.0;
+      }
+    }
+    fsync<NT>();
+  }
 
   // ------------------------------------------------ interior point
   int it = 0;
-  bool done = false;
   while (!done && it < IPM_MAX_IT) {
     ++it;
     gradient();
@@ -893,19 +930,11 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       // U is overwritten by the polish: keep the IPM iterate
       for (int e = lane; e < N * NU; e += NT) sm.Us[e / NU][e % NU] = sm.U[e / NU][e % NU];
       fsync<NT>();
-      for (int corr = 0; corr <= IPM_NCORR; ++corr) {
-        int changed = 0;
-        for (int j = lane; j < S; j += NT) FPREV(j) = FACT(j);
-        fsync<NT>();
-        if (polish()) {
-          done = true;
-          status = MPCQP_STATUS_OK;
-          break;
-        }
-        for (int j = lane; j < S; j += NT) changed |= FACT(j) != FPREV(j);
-        if (!__any(changed)) break;
+      if (polish_corrected()) {
+        done = true;
+        status = MPCQP_STATUS_OK;
+        break;
       }
-      if (done) break;
       for (int e = lane; e < N * NU; e += NT) sm.U[e / NU][e % NU] = sm.Us[e / NU][e % NU];
       fsync<NT>();
     }
@@ -996,6 +1025,16 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
   for (int e = lane; e < N * NU; e += NT) finite &= isfinite(sm.U[e / NU][e % NU]);
   if (__any(!finite)) status = MPCQP_STATUS_NONFINITE;
   if (lane < 12) u0g[(size_t)b * 12 + lane] = (float)sm.U[0][lane];
+  if (wmem) {   // remember the verified set (0x80 | rows; swing foot-steps 0x80), or nothing
+    const bool ok = status == MPCQP_STATUS_OK;
+    unsigned char* const wb = reinterpret_cast<unsigned char*>(&sm.rhs[0][0]);   // free from here on
+    for (int e = lane; e < MPCQP_WARM_BYTES; e += NT) wb[e] = ok && e < 4 * N ? 0x80 : 0;
+    fsync<NT>();
+    if (ok)
+      for (int j = lane; j < S; j += NT) wb[4 * sm.mt.foot_t[j] + sm.mt.foot_leg[j]] = (unsigned char)(0x80 | (FACT(j) & liv));
+    fsync<NT>();
+    for (int e = lane; e < MPCQP_WARM_BYTES; e += NT) wmem[e] = wb[e];
+  }
 #ifdef MPCQP_IPM_DEBUG
   {   // the last 8 slots: cycles in gradient / factor / lsolve / total, factor T / GJ / S store / sym
     const unsigned long long tot = __builtin_amdgcn_s_memtime() - cyc_t0;

@@ -115,6 +115,9 @@ class ModelPredictiveController():
             e = LinearMpc(horizon=self.horizon, robot=self._robot_record, dt=self.dt,
                           Q=self.Q, R=self.R, device=os.environ.get("MPCQP_DEVICE", "cuda:0"))
             e.set_planner(dt_control=self.dt_control, gravity=self.gravity)
+            # one robot solved every MPC tick: start from the previous tick's active set
+            # (the interior-point class only; the optimum is checked either way)
+            e.set_warm_start(0 if os.environ.get("MPCQP_COLD") else 1)
             d, f32 = e.device, dict(dtype=torch.float32, device=e.device)
             N = self.horizon
             self._dev = dict(

@@ -33,6 +33,7 @@ EXPORTED_SYMBOLS = (
     "mpcqp_set_stance_hint",
     "mpcqp_set_stance_range",
     "mpcqp_set_weights",
+    "mpcqp_set_warm_start",
     "mpcqp_destroy",
     "mpcqp_last_error",
     "mpcqp_plan",
@@ -40,7 +41,8 @@ EXPORTED_SYMBOLS = (
     "mpcqp_set_planner",
     "mpcqp_stance_torques",
 )
-ABI_VERSION = 4
+ABI_VERSION = 5
+WARM_BYTES = 128     # MPCQP_WARM_BYTES: warm-start memory per robot
 PLAN_STRIDE = 8     # MPCQP_PLAN_STRIDE: float64 planner state per robot
 GAIT_STRIDE = 9     # MPCQP_GAIT_STRIDE: period, offsets[4], durations[4]
 PLAN_REFERENCE = 1      # MPCQP_PLAN_REFERENCE: build X_ref (+ gait table) this tick
@@ -89,6 +91,8 @@ def load():
     lib.mpcqp_set_stance_range.argtypes = [vp, i32, i32]
     lib.mpcqp_set_weights.restype = ctypes.c_int
     lib.mpcqp_set_weights.argtypes = [vp, vp, vp]
+    lib.mpcqp_set_warm_start.restype = ctypes.c_int
+    lib.mpcqp_set_warm_start.argtypes = [vp, vp, i32]
     lib.mpcqp_destroy.restype = ctypes.c_int
     lib.mpcqp_destroy.argtypes = [vp]
     lib.mpcqp_last_error.restype = ctypes.c_char_p

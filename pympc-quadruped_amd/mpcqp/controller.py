@@ -33,11 +33,12 @@ class BatchedController:
       iterations_between_mpc: linear_mpc_configs.py:7 (20)
       dt_control: linear_mpc_configs.py:6 (0.001)
       height:   desired CoM height(s) (robot_configs.py:23,42); default from the preset
+      warm_start: remember each robot's active set between MPC ticks (LinearMpc.set_warm_start)
     """
 
     def __init__(self, batch, horizon=16, robot="aliengo", gait="trot10", iterations_between_mpc=20,
                  dt_control=0.001, gravity=9.81, height=None, dt=DT_MPC, Q=Q_DIAG, R=R_DIAG,
-                 device="cuda:0", max_iter=0, max_stance=0):
+                 device="cuda:0", max_iter=0, max_stance=0, warm_start=True):
         self.B = int(batch)
         self.N = int(horizon)
         self.iterations_between_mpc = int(iterations_between_mpc)
@@ -45,6 +46,8 @@ class BatchedController:
         self.engine = LinearMpc(horizon=self.N, robot=None if per_robot else robot, dt=dt, Q=Q, R=R,
                                 device=device, max_iter=max_iter, max_stance=max_stance)
         self.engine.set_planner(dt_control=dt_control, gravity=gravity)
+        if warm_start:   # the fleet is solved tick after tick: remember each robot's active set
+            self.engine.set_warm_start(int(batch))
         dev = self.engine.device
         self.device = dev
         B, N = self.B, self.N

@@ -121,6 +121,23 @@ class LinearMpc:
             _lib.check(self._ctx, self.lib.mpcqp_set_stance_range(self._ctx, *rng), "set_stance_range")
             self._hint = rng
 
+    def set_warm_start(self, capacity):
+        """Remember each robot's verified active set between solves (include/mpcqp.h
+        mpcqp_set_warm_start): robot b of every later solve starts the interior-point class
+        (n > 128, e.g. Gait.STANDING at N = 16) from the rows its previous solve had active,
+        and runs the interior point only when they fail the KKT check.  For callers that
+        solve the same robots tick after tick; results do not depend on it.  ``capacity`` =
+        robots remembered (robot indices 0 .. capacity - 1), 0 disables.  Returns the
+        engine-owned device memory (uint8 [capacity, WARM_BYTES]); zero it to forget."""
+        cap = int(capacity)
+        if cap < 0:
+            raise ValueError("capacity must be >= 0")
+        mem = torch.zeros((cap, _lib.WARM_BYTES), dtype=torch.uint8, device=self.device) if cap else None
+        _lib.check(self._ctx, self.lib.mpcqp_set_warm_start(self._ctx, mem.data_ptr() if cap else None, cap),
+                   "mpcqp_set_warm_start")
+        self._warm = mem   # the context holds its pointer: keep it alive
+        return mem
+
     def __del__(self):
         ctx = getattr(self, "_ctx", None)
         if ctx is not None and ctx.value:

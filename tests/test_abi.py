@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     lib = _lib.load()
     for name in _declared():
         assert hasattr(lib, name), name
-    assert lib.mpcqp_abi_version() == _lib.ABI_VERSION == 4
+    assert lib.mpcqp_abi_version() == _lib.ABI_VERSION == 5
 
 
 def test_params_struct_layout():
@@ -58,6 +58,7 @@ def test_create_rejects_bad_arguments_without_crashing():
     assert lib.mpcqp_plan_root_states(None, 1, 1, *([None] * 11)) == -1
     assert lib.mpcqp_stance_torques(None, 1, None, None, 4, None, None, None) == -1
     assert lib.mpcqp_set_planner(None, 0.001, 9.81, 0.1) == -1
+    assert lib.mpcqp_set_warm_start(None, None, 0) == -1
     assert lib.mpcqp_destroy(None) == 0
 
 
@@ -71,6 +72,7 @@ def test_header_constants_match_binding():
     assert int(consts["MPCQP_PLAN_REFERENCE"]) == _lib.PLAN_REFERENCE
     assert int(consts["MPCQP_PLAN_NO_INTEGRATE"]) == _lib.PLAN_NO_INTEGRATE
     assert int(consts["MPCQP_ROBOT_STRIDE"]) == _lib.ROBOT_STRIDE
+    assert int(consts["MPCQP_WARM_BYTES"]) == _lib.WARM_BYTES == 4 * _lib.MAX_HORIZON
 
 
 def test_horizon_limit_is_the_create_limit():

@@ -360,6 +360,51 @@ def test_long_horizons_interior_point(N):
     assert iters[0] > 0   # Newton factorisations: the interior-point class solved it
 
 
+@pytest.mark.parametrize("N", [16, 24])
+def test_warm_start_interior_point(N):
+    """mpcqp_set_warm_start: a fleet solved tick after tick (x0 drifting by a few mm / mrad
+    per tick) with each robot's previous active set remembered -- every tick's u0 and U
+    against the float64 oracle, statuses OK, and the warm interior-point robots needing
+    fewer Newton factorisations than the cold engine.  Then the memory is scrambled
+    (every robot handed another robot's set): still the oracle's optimum, since a set
+    that fails the KKT check is corrected or abandoned for the cold start."""
+    import torch
+    from mpcqp.synthetic import make_batch
+    B = 8
+    bt = make_batch(B, N, seed=500 + N, gaits=("trot10", "pace10", "bound8"), robots=("a1", "aliengo"))
+    bt["contact"][:6] = 1.0   # six standing robots (the interior-point class), two gait robots
+    warm, cold = _engine(N), _engine(N)
+    mem = warm.set_warm_start(B)
+    assert mem.shape == (B, 128) and int(mem.sum()) == 0
+    rng = np.random.default_rng(600 + N)
+    fw, fc = [], []
+    for tick in range(4):
+        if tick:
+            bt["x0"][:, :12] += rng.normal(0.0, 2e-3, size=(B, 12)).astype(np.float32)
+        u0, U, status, iters = _solve(warm, bt)
+        _, _, status_c, iters_c = _solve(cold, bt)
+        assert (status == 0).all() and (status_c == 0).all(), (tick, status, status_c)
+        for b in range(B):
+            x, _, _ = oracle_solution(bt, b, N)
+            e = max(rel_err_u0(u0[b], x[:12]), rel_err_u0(U[b], x))
+            assert e < TOL_ACHIEVED_IPM, (tick, b, e)
+        if tick:
+            fw.append(iters[:6].sum())
+            fc.append(iters_c[:6].sum())
+        m = mem.cpu().numpy()
+        assert np.all(m[:6, :4 * N] & 0x80) and np.all(m[:, 4 * N:] == 0), tick   # verified sets remembered
+    assert sum(fw) < sum(fc), (fw, fc)
+    # scrambled memory: robot b gets robot b + 1's set
+    mem.copy_(torch.roll(mem, 1, dims=0))
+    bt["x0"][:, :12] += rng.normal(0.0, 2e-2, size=(B, 12)).astype(np.float32)
+    u0, U, status, _ = _solve(warm, bt)
+    assert (status == 0).all(), status
+    for b in range(B):
+        x, _, _ = oracle_solution(bt, b, N)
+        assert max(rel_err_u0(u0[b], x[:12]), rel_err_u0(U[b], x)) < TOL_ACHIEVED_IPM, b
+    warm.set_warm_start(0)
+
+
 def test_stance_range_direct_classes():
     """mpcqp_set_stance_range: when the range rules out the smaller classes, the first
     possible class takes the batch directly -- the same kernels and arithmetic as the

@@ -35,6 +35,10 @@ MU_FLOOR = float(os.environ.get("MU_FLOOR", "1e-13"))   # centring target floor
 NREF = int(os.environ.get("NREF", "2"))                 # Newton refinements in the polish
 NCORR = int(os.environ.get("NCORR", "8"))               # active-set corrections per polish
 STAT_TOL = float(os.environ.get("STAT_TOL", "1e-10"))
+EARLY_CHG = int(os.environ.get("EARLY_CHG", "1000000"))  # give up once a correction changes more rows
+EARLY_MAXV = int(os.environ.get("EARLY_MAXV", "1000000"))  # only when the start violates <= this many rows
+EARLY = int(os.environ.get("EARLY", "-1"))              # >= 0: polish from the start point's violated
+                                                        # rows first, with this many corrections
 MAX_IT = int(os.environ.get("MAX_IT", "60"))
 
 
@@ -98,6 +102,7 @@ def solve(Ad, Bd, x0, xref, contact, N, mu, fz_max, normal, q_diag=F.Q_DIAG, r_d
 
     def gradient(U):
         """H U + g (stance coordinates) by a forward simulation and the adjoint."""
+        cnt["gradient"] += 1
         X = np.zeros((N + 1, 13))
         X[0] = x0
         for k in range(N):
@@ -109,7 +114,10 @@ def solve(Ad, Bd, x0, xref, contact, N, mu, fz_max, normal, q_diag=F.Q_DIAG, r_d
             gr[k] = Rh * U[k] + B.T @ nu
         return gr * np.repeat(stance, 3, axis=1)
 
+    cnt = {"factor": 0, "lsolve": 0, "gradient": 0}
+
     def factor(Bl, Ri):
+        cnt["factor"] += 1
         """S_k = (I + P_{k+1} E_k)^-1 P_{k+1}; Bl (N,4,13,3), Ri (N,4,3,3)."""
         S = np.zeros((N, 13, 13))
         P = np.diag(Qh)
@@ -121,6 +129,7 @@ def solve(Ad, Bd, x0, xref, contact, N, mu, fz_max, normal, q_diag=F.Q_DIAG, r_d
         return S
 
     def lsolve(Bl, Ri, S, rhs):
+        cnt["lsolve"] += 1
         """(H + per-leg Rt - Rh) d = rhs on the legs' subspaces (Bl already projected)."""
         p = np.zeros(13)
         Y = np.zeros((N, 4, 3))
@@ -217,6 +226,19 @@ def solve(Ad, Bd, x0, xref, contact, N, mu, fz_max, normal, q_diag=F.Q_DIAG, r_d
     # start: minimiser under a mild barrier weight, slacks shifted into the interior
     Bl, Ri = ipm_blocks(np.full((nf, R), 1e-2))
     U = lsolve(Bl, Ri, factor(Bl, Ri), -g0)
+    act = (fview(U) @ G.T - h) < 0
+    solve.nviol = int(act.sum())
+    if EARLY >= 0 and solve.nviol <= EARLY_MAXV:
+        for corr in range(EARLY + 1):
+            u, info, nact = polish(act)
+            if verbose:
+                print(f"   early polish {corr}: {info}")
+            if u is not None:
+                solve.cnt = cnt
+                return u, 0, nf, True
+            if np.array_equal(nact, act) or int((nact != act).sum()) > EARLY_CHG:
+                break
+            act = nact
     s = np.maximum(fview(U) @ G.T - h, 1.0)
     lam = np.ones((nf, R))
     polish_tries = 0
@@ -234,6 +256,7 @@ def solve(Ad, Bd, x0, xref, contact, N, mu, fz_max, normal, q_diag=F.Q_DIAG, r_d
                 if verbose:
                     print(f"   polish {polish_tries}.{corr}: {info}")
                 if u is not None:
+                    solve.cnt = cnt
                     return u, it, nf, True
                 if np.array_equal(nact, act):
                     break
@@ -257,6 +280,7 @@ def solve(Ad, Bd, x0, xref, contact, N, mu, fz_max, normal, q_diag=F.Q_DIAG, r_d
         U = U + ap * dU
         s = s + ap * ds
         lam = lam + ad * dl
+    solve.cnt = cnt
     return U, MAX_IT, nf, False
 
 
