@@ -41,6 +41,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="config2", choices=sorted(CONFIGS) + ["config1"])
+    ap.add_argument("--warm-fleet", action="store_true",
+                    help="a fleet solved tick after tick: the batches are a drift sequence (x0 + N(0, 2e-3) "
+                         "per tick, visited 0 1 2 3 2 1 ...) and the engine remembers each robot's active set "
+                         "(LinearMpc.set_warm_start); an extra line, never the headline")
     ap.add_argument("--standing-every", type=int, default=0,
                     help="diagnostics: make every k-th robot stand (the interior-point class)")
     ap.add_argument("--gait", default="trot10",
@@ -430,11 +434,25 @@ def main():
     if args.standing_every:
         for h in host:
             h["contact"][::args.standing_every] = 1.0
+    if args.warm_fleet:   # consecutive ticks of one fleet: each batch the previous one drifted
+        rng = np.random.default_rng(77 + rank)
+        for k in range(1, nbat):
+            h = {kk: v.copy() for kk, v in host[k - 1].items()}
+            h["x0"][:, :12] += rng.normal(0.0, 2e-3, size=(Bpg, 12)).astype(np.float32)
+            host[k] = h
+
+    def bi(k):   # the batch of step k: cycled, or ping-pong along the drift sequence
+        if not args.warm_fleet:
+            return k % nbat
+        j = k % (2 * nbat - 2)
+        return j if j < nbat else 2 * nbat - 2 - j
     # the caller knows its contact schedules: promise the largest stance count so the
     # engine launches only the capacity classes the workload can reach
     max_stance = int(max((h["contact"] > 0).reshape(Bpg, -1).sum(1).max() for h in host))
     eng = LinearMpc(horizon=N, robot=robots[0], device=dev, max_iter=args.max_iter,
                     max_stance=max_stance)
+    if args.warm_fleet:
+        eng.set_warm_start(Bpg)
     dev_b = []
     for h in host:
         dev_b.append({k: torch.as_tensor(v).to(dev).contiguous() for k, v in h.items()})
@@ -445,11 +463,11 @@ def main():
     gather_events = []
 
     def step(k, ev=None):
-        d = dev_b[k % nbat]
+        d = dev_b[bi(k)]
         if ev is not None:
             ev[0].record(stream)
         eng.solve_raw(Bpg, d["x0"], d["xref"], d["contact"], d["feet"], d["robot"], u0,
-                      None, status[k % nbat], iters[k % nbat], stream=stream)
+                      None, status[bi(k)], iters[bi(k)], stream=stream)
         if ev is not None:
             ev[1].record(stream)
         if world > 1 and not args.no_gather:
@@ -517,7 +535,7 @@ def main():
         exec_launch.append(sum(executed_flops(N, int(n), k) for n, k in zip(ns, ki)))
         it_all.append(it)
     st = np.concatenate([x.cpu().numpy() for x in status])   # every batch's last solve
-    steps_per_bat = [sum(1 for s in range(args.steps) if s % nbat == k) for k in range(nbat)]
+    steps_per_bat = [sum(1 for s in range(args.steps) if bi(s) == k) for k in range(nbat)]
     F_avg = sum(f * c for f, c in zip(flops_launch, steps_per_bat)) / args.steps
     E_avg = sum(f * c for f, c in zip(exec_launch, steps_per_bat)) / args.steps
     kavg_s = sum(kern_ms) / len(kern_ms) / 1e3
@@ -558,7 +576,7 @@ def main():
     # the default caller path (no stance promise: every capacity class launched, the idle
     # workgroups of the queued classes exit at once), timed the same way, outside `value`
     no_hint = None
-    if not args.no_hint_line and world == 1:
+    if not args.no_hint_line and not args.warm_fleet and world == 1:
         eng.set_stance_range(0, 0)
         for k in range(5):
             step(k)
@@ -581,7 +599,7 @@ def main():
     # launch's tail (its slowest robots, most CUs idle) overlaps the next launch's start.
     # Outside `value`, which keeps one batch at a time (a control loop's dependency).
     two_streams = None
-    if not args.no_hint_line and world == 1:
+    if not args.no_hint_line and not args.warm_fleet and world == 1:
         s2 = [stream, torch.cuda.Stream(dev)]
         u0s = [u0, torch.empty_like(u0)]
         sts = [torch.empty((Bpg,), dtype=torch.int32, device=dev) for _ in range(2)]
@@ -654,6 +672,10 @@ def main():
             line["gather_ms_avg"] = gather_ms
         if args.standing_every:
             line["config"]["workload"] += f", every {args.standing_every}th robot standing"
+        if args.warm_fleet:
+            line["config"]["workload"] += (", warm fleet: consecutive ticks of one fleet (x0 drifting "
+                                           "N(0, 2e-3) per tick), each robot's active set remembered")
+            line["data"] += "; warm start (mpcqp_set_warm_start): not comparable with the cold lines"
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

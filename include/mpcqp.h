@@ -22,10 +22,10 @@
  * negative error code; mpcqp_last_error() describes the last failure.
  * Per-robot solver outcome is reported in status[] (MPCQP_STATUS_*).
  * A context keeps per-stream device queues for up to 8 streams; a solve on a 9th
- * distinct stream takes over the least recently used stream's queues after a whole-
- * device synchronisation (hipDeviceSynchronize: it waits for every stream, and fails
- * while a stream is being captured into a graph).  Round-robin over at most 8 streams
- * per context to stay asynchronous.
+ * distinct stream takes over the least recently used stream's queues once that stream's
+ * last solve on this context has finished (the host waits on an event recorded after
+ * it -- not on the device or the other streams).  Round-robin over at most 8 streams per
+ * context to stay fully asynchronous.
  *
  * Layouts (float32, row-major, robot-major):
  *   x0      [B][13]   [roll, pitch, yaw, px, py, pz, wx, wy, wz, vx, vy, vz, -g]

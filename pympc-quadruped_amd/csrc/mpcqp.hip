@@ -515,6 +515,7 @@ struct QueueSet {
   hipEvent_t ev_fork, ev_join;
   double* sscratch;   // the interior-point class's Riccati S_k, one slot per workgroup (first use)
   int sslots;
+  hipEvent_t ev_done;   // recorded on `stream` after each call's last launch (eviction waits on it)
 };
 
 // Releases a queue set's device resources (the caller has synchronised the device).
@@ -522,6 +523,8 @@ static void release_set(QueueSet& q) {
   if (q.buf) (void)hipFree(q.buf);
   if (q.ev_fork) (void)hipEventDestroy(q.ev_fork);
   if (q.ev_join) (void)hipEventDestroy(q.ev_join);
+  if (q.ev_done) (void)hipEventDestroy(q.ev_done);
+  q.ev_done = nullptr;
   if (q.side) (void)hipStreamDestroy(q.side);
   if (q.sscratch) (void)hipFree(q.sscratch);
   q.sscratch = nullptr;
@@ -569,8 +572,9 @@ struct DeviceScope {
 };
 
 // At most this many streams keep a queue set; a new stream beyond them takes over the
-// least recently used set (after a device synchronisation: its stream may still run
-// launches that use it, and may already have been destroyed by the caller).
+// least recently used set with its buffers, once the event recorded after that set's last
+// call has completed (its stream may still run launches that use it, and may already have
+// been destroyed by the caller: the event outlives it).  No device-wide synchronisation.
 constexpr int kMaxQueueSets = 8;
 
 // The queue set of `st`, holding at least `batch` robots per queue (grown on demand;
@@ -589,17 +593,24 @@ static QueueSet* stream_queues(mpcqp_ctx* ctx, hipStream_t st, int batch, int* e
     QueueSet* lru = &ctx->queues[0];
     for (auto& q : ctx->queues)
       if (q.used < lru->used) lru = &q;
-    if (hipDeviceSynchronize() != hipSuccess) {
-      *err = set_err(ctx, MPCQP_ERR_HIP, "queue eviction: device sync failed");
+    if (lru->ev_done && hipEventSynchronize(lru->ev_done) != hipSuccess) {
+      *err = set_err(ctx, MPCQP_ERR_HIP, "queue eviction: event sync failed");
       return nullptr;
     }
-    release_set(*lru);
-    *lru = QueueSet{st, 0, nullptr, ++ctx->use_clock, nullptr, nullptr, nullptr, nullptr, 0};
+    // every launch that used the set is done: its queues are back at rest (each kernel
+    // resets its header) and its S_k slots free -- the new stream reuses them as they are
+    lru->stream = st;
+    lru->used = ++ctx->use_clock;
     qs = lru;
   }
   if (!qs) {
-    ctx->queues.push_back(QueueSet{st, 0, nullptr, ++ctx->use_clock, nullptr, nullptr, nullptr, nullptr, 0});
+    ctx->queues.push_back(QueueSet{st, 0, nullptr, ++ctx->use_clock, nullptr, nullptr, nullptr, nullptr, 0, nullptr});
     qs = &ctx->queues.back();
+    if (hipEventCreateWithFlags(&qs->ev_done, hipEventDisableTiming) != hipSuccess) {
+      qs->ev_done = nullptr;
+      *err = set_err(ctx, MPCQP_ERR_HIP, "queue event creation failed");
+      return nullptr;
+    }
   }
   if (qs->buf) {
     if (hipStreamSynchronize(st) != hipSuccess) {
@@ -834,6 +845,7 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   } else if (fork && hipStreamWaitEvent(st, qs->ev_join, 0) != hipSuccess) {
     return set_err(ctx, MPCQP_ERR_HIP, "interior-point join failed");
   }
+  if (qs && hipEventRecord(qs->ev_done, st) != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, "queue event record failed");
   return MPCQP_OK;
 }
 

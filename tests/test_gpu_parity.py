@@ -294,6 +294,41 @@ def test_two_streams_no_host_sync():
             assert rel_err_u0(U[b], x) < TOL_U0, b
 
 
+def test_queue_set_eviction_beyond_eight_streams():
+    """A context keeps queues for 8 streams; solves round-robin over 11 streams make the
+    9th-11th take over the least recently used sets (after waiting on their last solve's
+    event, with their buffers reused) -- every stream's batch (trot / pace / bound routed
+    to class 96, standing robots to the interior-point class) still gives the oracle's
+    optimum, over two rounds so reused sets are used again."""
+    import torch
+    from mpcqp.synthetic import make_batch
+    N = 16
+    eng = _engine(N)
+    dev = torch.device("cuda:0")
+    streams = [torch.cuda.Stream() for _ in range(11)]
+    bts = []
+    for i in range(len(streams)):
+        bt = make_batch(24, N, seed=700 + i, gaits=("trot10", "pace10", "bound8"), robots=("a1",))
+        bt["contact"][i % 4::6] = 1.0
+        bts.append(bt)
+    ins = [{k: torch.as_tensor(v).to(dev) for k, v in bt.items()} for bt in bts]
+    torch.cuda.synchronize()
+    for rnd in range(2):
+        outs = []
+        for s, t in zip(streams, ins):
+            with torch.cuda.stream(s):
+                outs.append(eng.solve(t["x0"], t["xref"], t["contact"], t["feet"], robot=t["robot"],
+                                      return_all=True, stream=s))
+        torch.cuda.synchronize()
+        for i, (bt, res) in enumerate(zip(bts, outs)):
+            status = res.status.cpu().numpy()
+            assert (status == 0).all(), (rnd, i, status)
+            U = res.U.cpu().numpy().reshape(len(bt["x0"]), -1)
+            for b in (i % 4, 5, 23):
+                x, _, _ = oracle_solution(bt, b, N)
+                assert rel_err_u0(U[b], x) < TOL_U0, (rnd, i, b)
+
+
 @pytest.mark.parametrize("N", [10, 16, 20])
 def test_random_contact_patterns_every_class(N):
     """Arbitrary (not gait-table) contact patterns with per-robot mu, fz_max and tilted

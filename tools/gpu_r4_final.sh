@@ -19,6 +19,7 @@ for c in config3 config4 config5; do
   timeout -k 10 200 python3 bench.py --no-cpu --no-callers --config $c > $O/bench_$c.json || exit $?
 done
 timeout -k 10 200 python3 bench.py --no-cpu --no-callers --no-hint-line --config config4 --standing-every 1 --steps 10 --warmup 2 > $O/bench_config4_standing1.json || exit $?
+timeout -k 10 200 python3 bench.py --no-cpu --no-callers --no-hint-line --config config4 --standing-every 1 --warm-fleet --steps 12 --warmup 2 > $O/bench_config4_standing1_warm.json || exit $?
 timeout -k 10 200 python3 bench.py --no-cpu --no-callers --config config4 --standing-every 16 --steps 40 --warmup 4 > $O/bench_config4_standing16.json || exit $?
 timeout -k 10 300 python3 bench.py --no-cpu --no-callers --config config5 --standing-every 16 --steps 20 --warmup 2 > $O/bench_config5_standing16.json || exit $?
 timeout -k 10 200 python3 bench.py --config config1 --cpu-seconds 4 > $O/c1_trot.json || exit $?
