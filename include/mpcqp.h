@@ -115,9 +115,10 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
  * entries included).  Diagonal matrices select the diagonal fast path (equivalent to
  * setting q_diag / r_diag).  The weights are copied before the call returns; solves issued
  * before it are unaffected.  A failed call (error code) leaves the previous weights in
- * force.  Cost: when full weights were in force, the call synchronises the whole device
- * (hipDeviceSynchronize) before releasing their buffer -- do not call it while a stream
- * of this device is being captured into a graph.
+ * force.  The previous full-weight buffer is kept until mpcqp_destroy (solves in flight
+ * may still read it); only every 64th change synchronises the whole device
+ * (hipDeviceSynchronize) to release the kept buffers -- not while a stream of this
+ * device is being captured into a graph.
  * The interior-point class (robots with more than 128 stance variables) supports a full
  * Q and an R without cross-leg couplings (R[i][j] = 0 for legs i / 3 != j / 3); a robot of
  * that class under weights it does not support reports MPCQP_STATUS_UNSUPPORTED. */

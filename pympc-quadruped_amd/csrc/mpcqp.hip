@@ -545,6 +545,7 @@ struct mpcqp_ctx {
   double* wdev;       // full Q (13 x 13) then R (12 x 12) on the device (mpcqp_set_weights); nullptr: diagonal
   double q_full[13 * 13];   // the current weights as whole matrices (host copies: a NULL argument
   double r_full[12 * 12];   // of mpcqp_set_weights keeps that matrix, off-diagonal entries included)
+  std::vector<double*> retired;   // earlier full-weight buffers (in-flight solves may read them)
   unsigned char* warm;   // warm-start memory (caller-owned device buffer), mpcqp_set_warm_start
   int warm_cap;
   double dt_control;  // planner constants (mpcqp_set_planner)
@@ -576,6 +577,8 @@ struct DeviceScope {
 // call has completed (its stream may still run launches that use it, and may already have
 // been destroyed by the caller: the event outlives it).  No device-wide synchronisation.
 constexpr int kMaxQueueSets = 8;
+// Full-weight buffers retired by mpcqp_set_weights before one device-wide release.
+constexpr size_t kMaxRetired = 64;
 
 // The queue set of `st`, holding at least `batch` robots per queue (grown on demand;
 // the old buffer is freed once the stream's earlier launches are done).
@@ -895,13 +898,18 @@ int mpcqp_set_weights(mpcqp_ctx* ctx, const double* Q, const double* R) {
     }
   }
   // launches on any stream (non-blocking ones included) may still read the previous
-  // buffer: it is released after a device synchronisation (the cost of a weight change)
+  // buffer: it is retired, not freed (2.5 KB each), and released at mpcqp_destroy -- or,
+  // past kMaxRetired changes, all at once after a device synchronisation
   if (ctx->wdev) {
-    if (hipDeviceSynchronize() != hipSuccess) {
-      if (nb) (void)hipFree(nb);
-      return set_err(ctx, MPCQP_ERR_HIP, "weights: device sync failed");
+    if (ctx->retired.size() >= kMaxRetired) {
+      if (hipDeviceSynchronize() != hipSuccess) {
+        if (nb) (void)hipFree(nb);
+        return set_err(ctx, MPCQP_ERR_HIP, "weights: device sync failed");
+      }
+      for (double* o : ctx->retired) (void)hipFree(o);
+      ctx->retired.clear();
     }
-    (void)hipFree(ctx->wdev);
+    ctx->retired.push_back(ctx->wdev);
   }
   ctx->wdev = nb;   // nullptr: the diagonal fast path (the weights live in the kernel arguments)
   memcpy(ctx->q_full, q, sizeof(q));
@@ -996,6 +1004,7 @@ int mpcqp_destroy(mpcqp_ctx* ctx) {
     // (a recorded stream may already have been destroyed by the caller)
     for (auto& q : ctx->queues) release_set(q);
     if (ctx->wdev) (void)hipFree(ctx->wdev);
+    for (double* o : ctx->retired) (void)hipFree(o);
   }
   delete ctx;
   return MPCQP_OK;
