@@ -524,6 +524,7 @@ def main():
     flops_launch = []
     exec_launch = []
     it_all = []
+    n_ipm = 0
     for k in range(nbat):
         it = iters[k].cpu().numpy()
         ns = 3 * (host[k]["contact"] > 0).reshape(Bpg, -1).sum(1)
@@ -531,6 +532,7 @@ def main():
         # active-set steps: such robots are priced at the formulation + one n^3/3
         # factorisation only (K = 0), a lower bound on their work
         ki = [0 if n > 128 else int(i) for n, i in zip(ns, it)]
+        n_ipm += int((ns > 128).sum())
         flops_launch.append(sum(algorithmic_flops(N, int(n), k) for n, k in zip(ns, ki)))
         exec_launch.append(sum(executed_flops(N, int(n), k) for n, k in zip(ns, ki)))
         it_all.append(it)
@@ -664,6 +666,12 @@ def main():
         }
         if traffic_note:
             line["roofline"]["traffic_note"] = traffic_note
+        if n_ipm:
+            line["roofline"]["note"] = (
+                f"{n_ipm} of {nbat * Bpg} robots have n > 128 (the interior-point class): they are priced at "
+                "the reference's dense formulation + one n^3/3 factorisation, work that class never executes "
+                "(it solves the uncondensed horizon by Riccati recursions), so frac / executed_frac of this "
+                "line are reference-work rates, not hardware utilisation")
         if no_hint is not None:
             line["no_hint"] = no_hint
         if two_streams is not None:
