@@ -474,7 +474,7 @@ __global__ __launch_bounds__(LANES) void mpcqp_kernel_ipm(
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
     int* __restrict__ queue, int direct_B, double* __restrict__ sscratch, unsigned* __restrict__ sbits,
     int nsw) {
-  __shared__ IpmSharedT<NM> sm;
+  __shared__ IpmSharedT<NM, FULL> sm;
   const int tid = threadIdx.x;
   const int k = blockIdx.x;
   // direct_B > 0: the caller's stance range (or N > 20) rules the dense classes out, robot = k

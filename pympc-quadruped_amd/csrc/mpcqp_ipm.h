@@ -65,21 +65,38 @@ struct IpmFootReg {
   int fact, fprev;
 };
 
-// LDS of one robot, sized for horizons N <= NM: NM = 16 (the reference's default horizon)
-// takes 52 KB -- three robots per CU --, NM = 20 one robot per CU.  The Riccati S_k live in
-// a per-workgroup global scratch slot (read only by lsolve's batched phases); the
-// formulation scratch shares its space with M_k and the gradient's / lsolve's per-stage
-// temporaries, which are first written after it is dead.
+// LDS of one robot, sized for horizons N <= NM.  NM = 16 (the reference's default horizon):
+// 40 KB with diagonal weights -- four robots per CU, one wave per SIMD --, 43 KB with full
+// ones (three); NM = 20 / 32 one robot per CU.  The Riccati S_k always live in a
+// per-workgroup global scratch slot (read only by lsolve's batched phases); at NM = 16 the
+// slot also holds M_k and its transpose (read row by row in lsolve's two recursions, the
+// next stage's row loaded under the current stage's work) and the saved IPM iterate.  The
+// formulation scratch shares its space with the per-stage temporaries (and M_k when it is
+// in LDS), which are first written after it is dead.
+struct IpmEmpty {};
 template <int NM>
+struct IpmMLds {
+  alignas(16) double M[NM][144];   // M_k = A^T (I - S_k E_k): lsolve's stage maps (row-major)
+};
+template <int NM>
+struct IpmUsLds {
+  alignas(16) double Us[NM][NU];   // the IPM iterate while a polish overwrites U
+};
+struct IpmWFull {
+  double qf[NX][NX];               // Qh = 2 Q (full)
+  double rf[NU][NU];               // Rh = 2 R (leg blocks used)
+};
+template <int NM, bool FULL>
 struct alignas(16) IpmSharedT {
   static constexpr int IPM_NF = 4 * NM;
+  static constexpr bool kMG = NM <= 16;   // M_k, M_k^T and the saved iterate in the global slot
   union {
     struct {
       FormT<NM> f;
       FormY fy;
     } fa;                          // formulation scratch (dead once Bm / x0 / xr are copied)
     struct {
-      alignas(16) double M[NM][144];   // M_k = A^T (I - S_k E_k): lsolve's stage maps (row-major)
+      [[no_unique_address]] std::conditional_t<kMG, IpmEmpty, IpmMLds<NM>> mk;
       union {
         struct {                       // gradient() temporaries
           alignas(16) double X[NM + 1][16];
@@ -105,21 +122,23 @@ struct alignas(16) IpmSharedT {
   double xr[NM][NX];               // xref, float64
   double qh[16];                   // 2 q
   double rh[NU];                   // 2 r
-  double qf[NX][NX];               // Qh = 2 Q (full; the diagonal case fills the diagonal)
-  double rf[NU][NU];               // Rh = 2 R (leg blocks used)
+  [[no_unique_address]] std::conditional_t<FULL, IpmWFull, IpmEmpty> wf;   // full weights only
   double W[IPM_NF][9];             // per stance foot-step 3x3 weight of the Newton system
   alignas(16) double P[144];       // P_{k+1}
   alignas(16) double U[NM][NU];    // iterate (swing entries 0)
   alignas(16) double dU[NM][NU];
   alignas(16) double rhs[NM][NU];
   alignas(16) double gr[NM][NU];
-  alignas(16) double Us[NM][NU];   // the IPM iterate while a polish overwrites U
+  [[no_unique_address]] std::conditional_t<kMG, IpmEmpty, IpmUsLds<NM>> us;
   // per stance foot-step interior-point state in LDS when a lane owns more than one
   // foot-step (NM > 16); with at most 64 foot-steps each lane keeps its one in registers
   std::conditional_t<(IPM_NF > LANES), IpmFootLds<IPM_NF>, IpmFootNone> ft;
 };
-// the Riccati S_k of one robot in its workgroup's global scratch slot
-constexpr int IPM_S_SLOT = kMaxN * 144;   // doubles per slot
+static_assert(sizeof(IpmSharedT<16, false>) <= 160 * 1024 / 4, "N <= 16, diagonal weights: four robots per CU");
+static_assert(sizeof(IpmSharedT<16, true>) <= 160 * 1024 / 3, "N <= 16, full weights: three robots per CU");
+// one robot's global slot: S_k, then (NM <= 16) M_k, M_k^T and the saved iterate
+constexpr int IPM_SLOT_S = 0, IPM_SLOT_M = kMaxN * 144, IPM_SLOT_MT = 2 * kMaxN * 144, IPM_SLOT_US = 3 * kMaxN * 144;
+constexpr int IPM_S_SLOT = 3 * kMaxN * 144 + kMaxN * NU;   // doubles per slot
 
 // 12 consecutive doubles of a 16-B aligned LDS vector, 16 B per read
 __device__ __forceinline__ void ld12(double (&v)[12], const double* p) {
@@ -175,7 +194,7 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 
 // One robot with more than 128 stance variables.  Called by a 64-thread workgroup.
 template <bool FULL, int NM>
-__device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSharedT<NM>& sm, double* __restrict__ Sg,
+__device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSharedT<NM, FULL>& sm, double* __restrict__ Sg,
                                                 const float* __restrict__ x0g, const float* __restrict__ xrefg,
                                                 const float* __restrict__ contactg, const float* __restrict__ feetg,
                                                 const float* __restrict__ robotg, float* __restrict__ u0g,
@@ -234,8 +253,8 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     }
     if (lane < NU) sm.rh[lane] = 2.0 * KP.r[lane];
     if constexpr (FULL) {
-      for (int e = lane; e < NX * NX; e += NT) sm.qf[e / NX][e % NX] = 2.0 * KP.wfull[e];
-      for (int e = lane; e < NU * NU; e += NT) sm.rf[e / NU][e % NU] = 2.0 * KP.wfull[NX * NX + e];
+      for (int e = lane; e < NX * NX; e += NT) sm.wf.qf[e / NX][e % NX] = 2.0 * KP.wfull[e];
+      for (int e = lane; e < NU * NU; e += NT) sm.wf.rf[e / NU][e % NU] = 2.0 * KP.wfull[NX * NX + e];
     }
     for (int e = lane; e < N * NX; e += NT) sm.xr[e / NX][e % NX] = (double)smf.in[FormT<NM>::IN_XREF + e];
     for (int e = lane; e < N * NU; e += NT) sm.U[e / NU][e % NU] = 0.0;
@@ -281,7 +300,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
 #pragma unroll
       for (int x = 0; x < 3; ++x)
 #pragma unroll
-        for (int y = 0; y < 3; ++y) o[3 * x + y] = sm.rf[3 * l + x][3 * l + y];
+        for (int y = 0; y < 3; ++y) o[3 * x + y] = sm.wf.rf[3 * l + x][3 * l + y];
     } else {
       o[0] = sm.rh[3 * l];
       o[1] = sm.rh[3 * l + 1];
@@ -371,7 +390,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       if constexpr (FULL) {
         if (lane < NX) {
 #pragma unroll
-          for (int j = 0; j < NX; ++j) v = fma(sm.qf[li][j], sm.X[k + 1][j] - sm.xr[k][j], v);
+          for (int j = 0; j < NX; ++j) v = fma(sm.wf.qf[li][j], sm.X[k + 1][j] - sm.xr[k][j], v);
         }
       } else {
         v = lane < NX ? sm.qh[li] * (sm.X[k + 1][li] - sm.xr[k][li]) : 0.0;
@@ -395,7 +414,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       double ru;
       if constexpr (FULL) {
         const int c3 = 3 * (c / 3);   // Rh's leg block (no cross-leg couplings in this class)
-        ru = fma(sm.rf[c][c3 + 2], sm.U[k][c3 + 2], fma(sm.rf[c][c3 + 1], sm.U[k][c3 + 1], sm.rf[c][c3] * sm.U[k][c3]));
+        ru = fma(sm.wf.rf[c][c3 + 2], sm.U[k][c3 + 2], fma(sm.wf.rf[c][c3 + 1], sm.U[k][c3 + 1], sm.wf.rf[c][c3] * sm.U[k][c3]));
       } else {
         ru = sm.rh[c] * sm.U[k][c];
       }
@@ -449,7 +468,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     d4 v;
     if constexpr (FULL) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = (lr + 4 * i < 12 && lc < 12) ? sm.qf[lr + 4 * i][lc] : 0.0;
+      for (int i = 0; i < 4; ++i) v[i] = (lr + 4 * i < 12 && lc < 12) ? sm.wf.qf[lr + 4 * i][lc] : 0.0;
     } else {
       v = diag4(sm.qh[lcc]);
     }
@@ -473,7 +492,8 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     }
     return Er;
   };
-  auto stage_m = [&](int k, const d4& Sr, const d4& Er) {   // M_k = (I + Nm^T) (I - S E) -> sm.M[k]
+  constexpr bool kMG = IpmSharedT<NM, FULL>::kMG;
+  auto stage_m = [&](int k, const d4& Sr, const d4& Er) {   // M_k = (I + Nm^T) (I - S E) -> M[k] (and M^T)
     d4 Lr = diag4(1.0);
 #pragma unroll
     for (int q = 0; q < 3; ++q) Lr = mfma(-Sr[q], Er[q], Lr);
@@ -483,7 +503,14 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = lr + 4 * i;
-      if (r < 12 && lc < 12) sm.M[k][12 * r + lc] = Mr[i];
+      if (r < 12 && lc < 12) {
+        if constexpr (kMG) {
+          Sg[IPM_SLOT_M + k * 144 + 12 * r + lc] = Mr[i];
+          Sg[IPM_SLOT_MT + k * 144 + 12 * lc + r] = Mr[i];
+        } else {
+          sm.mk.M[k][12 * r + lc] = Mr[i];
+        }
+      }
     }
   };
 
@@ -559,7 +586,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     }
     stage_m(0, Sp, Ep);
     fsync<NT>();   // S_k, M_k for lsolve
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // S_k's global stores, before lsolve reads them
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // the global stores (S_k, M_k), before lsolve reads them
     IPM_T1(1);
   };
 
@@ -634,15 +661,33 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     fsync<NT>();
     // backward recursion: lane i < 12 holds p_i
     double p = 0.0;
-    for (int k = N - 1; k >= 0; --k) {
-      if (lane < NU) sm.ph[k][lane] = p;
-      if (k > 0) {
-        double mr[12], r[12];
-        ld12(mr, sm.M[k] + 12 * l12);
-        const double ck = sm.lc[k][l12];
+    if constexpr (kMG) {   // row l12 of M_k from the global slot, the next stage's issued ahead
+      double mn[12];
+      if (N > 1) ld12g(mn, Sg + IPM_SLOT_M + (N - 1) * 144 + 12 * l12);
+      for (int k = N - 1; k >= 0; --k) {
+        if (lane < NU) sm.ph[k][lane] = p;
+        if (k > 0) {
+          double mr[12], r[12];
 #pragma unroll
-        for (int j = 0; j < 12; ++j) r[j] = readlane_d(p, j);
-        p = lane < NU ? dot12(mr, r) + ck : 0.0;
+          for (int j = 0; j < 12; ++j) mr[j] = mn[j];
+          if (k > 1) ld12g(mn, Sg + IPM_SLOT_M + (k - 1) * 144 + 12 * l12);
+          const double ck = sm.lc[k][l12];
+#pragma unroll
+          for (int j = 0; j < 12; ++j) r[j] = readlane_d(p, j);
+          p = lane < NU ? dot12(mr, r) + ck : 0.0;
+        }
+      }
+    } else {
+      for (int k = N - 1; k >= 0; --k) {
+        if (lane < NU) sm.ph[k][lane] = p;
+        if (k > 0) {
+          double mr[12], r[12];
+          ld12(mr, sm.mk.M[k] + 12 * l12);
+          const double ck = sm.lc[k][l12];
+#pragma unroll
+          for (int j = 0; j < 12; ++j) r[j] = readlane_d(p, j);
+          p = lane < NU ? dot12(mr, r) + ck : 0.0;
+        }
       }
     }
     fsync<NT>();
@@ -665,16 +710,34 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     bmat(sm.lc, sm.lb);   // B lb
     // forward recursion: lane i < 12 holds dx_i; dx_{k+1} = M_k^T dx_k + lc_k
     double dx = 0.0;
-    for (int k = 0; k < N; ++k) {
-      if (lane < NU) sm.dxh[k][lane] = dx;
-      if (k < N - 1) {
-        double mc[12], r[12];
+    if constexpr (kMG) {   // column l12 of M_k = row l12 of the stored transpose, issued ahead
+      double mn[12];
+      if (N > 1) ld12g(mn, Sg + IPM_SLOT_MT + 12 * l12);
+      for (int k = 0; k < N; ++k) {
+        if (lane < NU) sm.dxh[k][lane] = dx;
+        if (k < N - 1) {
+          double mc[12], r[12];
 #pragma unroll
-        for (int j = 0; j < 12; ++j) mc[j] = sm.M[k][12 * j + l12];
-        const double ek = sm.lc[k][l12];
+          for (int j = 0; j < 12; ++j) mc[j] = mn[j];
+          if (k < N - 2) ld12g(mn, Sg + IPM_SLOT_MT + (k + 1) * 144 + 12 * l12);
+          const double ek = sm.lc[k][l12];
 #pragma unroll
-        for (int j = 0; j < 12; ++j) r[j] = readlane_d(dx, j);
-        dx = lane < NU ? dot12(mc, r) + ek : 0.0;
+          for (int j = 0; j < 12; ++j) r[j] = readlane_d(dx, j);
+          dx = lane < NU ? dot12(mc, r) + ek : 0.0;
+        }
+      }
+    } else {
+      for (int k = 0; k < N; ++k) {
+        if (lane < NU) sm.dxh[k][lane] = dx;
+        if (k < N - 1) {
+          double mc[12], r[12];
+#pragma unroll
+          for (int j = 0; j < 12; ++j) mc[j] = sm.mk.M[k][12 * j + l12];
+          const double ek = sm.lc[k][l12];
+#pragma unroll
+          for (int j = 0; j < 12; ++j) r[j] = readlane_d(dx, j);
+          dx = lane < NU ? dot12(mc, r) + ek : 0.0;
+        }
       }
     }
     fsync<NT>();
@@ -928,14 +991,20 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
         FACT(j) = a;
       }
       // U is overwritten by the polish: keep the IPM iterate
-      for (int e = lane; e < N * NU; e += NT) sm.Us[e / NU][e % NU] = sm.U[e / NU][e % NU];
+      for (int e = lane; e < N * NU; e += NT) {
+        if constexpr (kMG) Sg[IPM_SLOT_US + e] = sm.U[e / NU][e % NU];
+        else sm.us.Us[e / NU][e % NU] = sm.U[e / NU][e % NU];
+      }
       fsync<NT>();
       if (polish_corrected()) {
         done = true;
         status = MPCQP_STATUS_OK;
         break;
       }
-      for (int e = lane; e < N * NU; e += NT) sm.U[e / NU][e % NU] = sm.Us[e / NU][e % NU];
+      for (int e = lane; e < N * NU; e += NT) {
+        if constexpr (kMG) sm.U[e / NU][e % NU] = Sg[IPM_SLOT_US + e];
+        else sm.U[e / NU][e % NU] = sm.us.Us[e / NU][e % NU];
+      }
       fsync<NT>();
     }
     for (int j = lane; j < S; j += NT) {
