@@ -449,8 +449,12 @@ def main():
     # the caller knows its contact schedules: promise the largest stance count so the
     # engine launches only the capacity classes the workload can reach
     max_stance = int(max((h["contact"] > 0).reshape(Bpg, -1).sum(1).max() for h in host))
+    min_stance = int(min((h["contact"] > 0).reshape(Bpg, -1).sum(1).min() for h in host))
     eng = LinearMpc(horizon=N, robot=robots[0], device=dev, max_iter=args.max_iter,
                     max_stance=max_stance)
+    # and the smallest: the first capacity class any robot needs takes the batch directly
+    # (mpcqp_set_stance_range; an all-standing fleet goes straight to the interior-point class)
+    eng.set_stance_range(min_stance, max_stance)
     if args.warm_fleet:
         eng.set_warm_start(Bpg)
     dev_b = []
@@ -596,7 +600,7 @@ def main():
                    "ms_per_step": nh_el / nh_steps * 1e3, "kernel_ms_avg": e0.elapsed_time(e1) / nh_steps,
                    "vs_hinted": (Bpg * nh_steps / nh_el) / qps,
                    "note": "LinearMpc(max_stance=0): the caller promises nothing about its schedules"}
-        eng.set_stance_hint(max_stance)
+        eng.set_stance_range(min_stance, max_stance)
     # a serving-style workload: independent batches alternating two HIP streams, so one
     # launch's tail (its slowest robots, most CUs idle) overlaps the next launch's start.
     # Outside `value`, which keeps one batch at a time (a control loop's dependency).
@@ -662,6 +666,7 @@ def main():
             "iters_mean": float(it_all.mean()),
             "iters_max": int(it_all.max()),
             "status_ok_frac": float((st == 0).mean()),
+            "stance_range": [min_stance, max_stance],
             "callers": callers,
         }
         if traffic_note:

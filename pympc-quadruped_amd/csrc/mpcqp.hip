@@ -467,14 +467,14 @@ __device__ __forceinline__ int ipm_claim_slot(unsigned* bits, int nw, int start)
 
 // Large class (n > 128, and every robot at N > 20): one wave per robot; its Riccati S_k in
 // a global slot claimed for the robot's solve (sbits: slot bitmap, nsw words)
-template <bool FULL, int NM>
+template <bool FULL, int NM, bool MG = false>
 __global__ __launch_bounds__(LANES) void mpcqp_kernel_ipm(
     KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
     int* __restrict__ queue, int direct_B, double* __restrict__ sscratch, unsigned* __restrict__ sbits,
     int nsw) {
-  __shared__ IpmSharedT<NM, FULL> sm;
+  __shared__ IpmSharedT<NM, FULL, MG> sm;
   const int tid = threadIdx.x;
   const int k = blockIdx.x;
   // direct_B > 0: the caller's stance range (or N > 20) rules the dense classes out, robot = k
@@ -485,7 +485,7 @@ __global__ __launch_bounds__(LANES) void mpcqp_kernel_ipm(
   int slot = 0;
   if (tid == 0) slot = ipm_claim_slot(sbits, nsw, k % nsw);
   slot = __builtin_amdgcn_readlane(slot, 0);
-  solve_robot_ipm<FULL, NM>(P, b, sm, sscratch + (size_t)slot * IPM_S_SLOT, x0g, xrefg, contactg, feetg, robotg, u0g,
+  solve_robot_ipm<FULL, NM, MG>(P, b, sm, sscratch + (size_t)slot * IPM_S_SLOT, x0g, xrefg, contactg, feetg, robotg, u0g,
                             Ug, statusg, itersg);
   if (tid == 0) {
     atomicAnd(&sbits[slot >> 5], ~(1u << (slot & 31)));   // the solve's S_k reads are done
@@ -762,7 +762,11 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   const bool ipm_only = kp.N > kDenseN;
   const bool large = ipm_only || nmax > kCap64, huge = !ipm_only && nmax > 96, giant = ipm_only || nmax > 128;
   // the first class launched: 0 = class 64, 1 = 96, 2 = 128, 3 = interior point
-  const int first = ipm_only ? 3 : nmin > 128 ? 3 : nmin > 96 ? 2 : nmin > kCap64 ? 1 : 0;
+  // When the interior-point class may be needed beside the dense ones, class 64 routes the
+  // batch (a formulation-stage pass, microseconds) so the interior-point launch forks onto
+  // its side stream at once -- a dense class taking the batch directly would route its
+  // standing robots only as its own workgroups run, and the fork would wait for all of it.
+  const int first = ipm_only || nmin > 128 ? 3 : giant ? 0 : nmin > 96 ? 2 : nmin > kCap64 ? 1 : 0;
   int* q = nullptr;
   QueueSet* qs = nullptr;
   int cap = 0;
@@ -795,7 +799,13 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   auto launch_ipm = [&](hipStream_t s) -> hipError_t {
     // the LDS layout for the horizon: N <= 16 (the reference's default) three robots per CU,
     // N <= 20 one, longer horizons (up to kMaxN) one
-    auto kern = kp.N <= 16       ? (full ? mpcqp_kernel_ipm<true, 16> : mpcqp_kernel_ipm<false, 16>)
+    // N <= 16: the throughput layout (four robots per CU, M_k in the global slot) when the
+    // class takes a batch larger than three robots per CU can hold at once; otherwise -- a
+    // single drop-in robot, or robots queued from a mixed batch, whose latency is the
+    // launch's tail -- the latency layout (M_k in LDS, three per CU)
+    const bool thru = first == 3 && batch > 3 * ctx->ncu;
+    auto kern = kp.N <= 16 ? (thru ? (full ? mpcqp_kernel_ipm<true, 16, true> : mpcqp_kernel_ipm<false, 16, true>)
+                                   : (full ? mpcqp_kernel_ipm<true, 16> : mpcqp_kernel_ipm<false, 16>))
                 : kp.N <= kDenseN ? (full ? mpcqp_kernel_ipm<true, kDenseN> : mpcqp_kernel_ipm<false, kDenseN>)
                                   : (full ? mpcqp_kernel_ipm<true, kMaxN> : mpcqp_kernel_ipm<false, kMaxN>);
     // one workgroup per robot of the batch (the queued ones beyond the count exit at once)

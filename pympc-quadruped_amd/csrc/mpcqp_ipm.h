@@ -66,10 +66,11 @@ struct IpmFootReg {
 };
 
 // LDS of one robot, sized for horizons N <= NM.  NM = 16 (the reference's default horizon):
-// 40 KB with diagonal weights -- four robots per CU, one wave per SIMD --, 43 KB with full
-// ones (three); NM = 20 / 32 one robot per CU.  The Riccati S_k always live in a
-// per-workgroup global scratch slot (read only by lsolve's batched phases); at NM = 16 the
-// slot also holds M_k and its transpose (read row by row in lsolve's two recursions, the
+// MG (throughput layout) 40 KB with diagonal weights -- four robots per CU, one wave per
+// SIMD --, 43 KB with full ones (three); without MG (latency layout, M_k in LDS) 52 KB,
+// three per CU; NM = 20 / 32 one robot per CU.  The Riccati S_k always live in a
+// per-workgroup global scratch slot (read only by lsolve's batched phases); with MG at NM = 16
+// the slot also holds M_k and its transpose (read row by row in lsolve's two recursions, the
 // next stage's row loaded under the current stage's work) and the saved IPM iterate.  The
 // formulation scratch shares its space with the per-stage temporaries (and M_k when it is
 // in LDS), which are first written after it is dead.
@@ -86,10 +87,10 @@ struct IpmWFull {
   double qf[NX][NX];               // Qh = 2 Q (full)
   double rf[NU][NU];               // Rh = 2 R (leg blocks used)
 };
-template <int NM, bool FULL>
+template <int NM, bool FULL, bool MG>
 struct alignas(16) IpmSharedT {
   static constexpr int IPM_NF = 4 * NM;
-  static constexpr bool kMG = NM <= 16;   // M_k, M_k^T and the saved iterate in the global slot
+  static constexpr bool kMG = MG && NM <= 16;   // M_k, M_k^T and the saved iterate in the global slot
   union {
     struct {
       FormT<NM> f;
@@ -134,8 +135,9 @@ struct alignas(16) IpmSharedT {
   // foot-step (NM > 16); with at most 64 foot-steps each lane keeps its one in registers
   std::conditional_t<(IPM_NF > LANES), IpmFootLds<IPM_NF>, IpmFootNone> ft;
 };
-static_assert(sizeof(IpmSharedT<16, false>) <= 160 * 1024 / 4, "N <= 16, diagonal weights: four robots per CU");
-static_assert(sizeof(IpmSharedT<16, true>) <= 160 * 1024 / 3, "N <= 16, full weights: three robots per CU");
+static_assert(sizeof(IpmSharedT<16, false, true>) <= 160 * 1024 / 4, "N <= 16, diagonal weights: four robots per CU");
+static_assert(sizeof(IpmSharedT<16, true, true>) <= 160 * 1024 / 3, "N <= 16, full weights: three robots per CU");
+static_assert(sizeof(IpmSharedT<16, true, false>) <= 160 * 1024 / 3, "N <= 16, M_k in LDS: three robots per CU");
 // one robot's global slot: S_k, then (NM <= 16) M_k, M_k^T and the saved iterate
 constexpr int IPM_SLOT_S = 0, IPM_SLOT_M = kMaxN * 144, IPM_SLOT_MT = 2 * kMaxN * 144, IPM_SLOT_US = 3 * kMaxN * 144;
 constexpr int IPM_S_SLOT = 3 * kMaxN * 144 + kMaxN * NU;   // doubles per slot
@@ -193,8 +195,8 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 }
 
 // One robot with more than 128 stance variables.  Called by a 64-thread workgroup.
-template <bool FULL, int NM>
-__device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSharedT<NM, FULL>& sm, double* __restrict__ Sg,
+template <bool FULL, int NM, bool MG>
+__device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSharedT<NM, FULL, MG>& sm, double* __restrict__ Sg,
                                                 const float* __restrict__ x0g, const float* __restrict__ xrefg,
                                                 const float* __restrict__ contactg, const float* __restrict__ feetg,
                                                 const float* __restrict__ robotg, float* __restrict__ u0g,
@@ -492,7 +494,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     }
     return Er;
   };
-  constexpr bool kMG = IpmSharedT<NM, FULL>::kMG;
+  constexpr bool kMG = IpmSharedT<NM, FULL, MG>::kMG;
   auto stage_m = [&](int k, const d4& Sr, const d4& Er) {   // M_k = (I + Nm^T) (I - S E) -> M[k] (and M^T)
     d4 Lr = diag4(1.0);
 #pragma unroll

@@ -294,6 +294,34 @@ def test_two_streams_no_host_sync():
             assert rel_err_u0(U[b], x) < TOL_U0, b
 
 
+def test_interior_point_throughput_layout():
+    """An all-standing batch larger than three robots per CU, promised as such
+    (mpcqp_set_stance_range(4N, 4N)): the interior-point class takes it directly in its
+    throughput layout (four robots per CU, M_k in the global slot) -- every status OK and
+    sampled robots against the oracle; the same robots through the latency layout (a small
+    batch) agree to the interior-point guard."""
+    import torch
+    from mpcqp.synthetic import make_batch
+    N = 16
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    B = 3 * ncu + 16
+    bt = make_batch(B, N, seed=910, gaits=("trot10",), robots=("a1", "aliengo"), tilt_deg=5.0)
+    bt["contact"][:] = 1.0
+    eng = _engine(N)
+    eng.set_stance_range(4 * N, 4 * N)
+    u0, U, status, iters = _solve(eng, bt)
+    assert (status == 0).all(), np.unique(status, return_counts=True)
+    assert (iters > 0).all()
+    pick = [0, 1, B // 2, B - 2, B - 1]
+    small = {k: v[pick] for k, v in bt.items()}
+    u0s, Us, sts, _ = _solve(_engine(N), small)
+    assert (sts == 0).all()
+    for j, b in enumerate(pick):
+        x, _, _ = oracle_solution(bt, b, N)
+        assert max(rel_err_u0(u0[b], x[:12]), rel_err_u0(U[b], x)) < TOL_ACHIEVED_IPM, b
+        assert rel_err_u0(U[b], Us[j].astype(np.float64)) < TOL_ACHIEVED_IPM, b
+
+
 def test_queue_set_eviction_beyond_eight_streams():
     """A context keeps queues for 8 streams; solves round-robin over 11 streams make the
     9th-11th take over the least recently used sets (after waiting on their last solve's
