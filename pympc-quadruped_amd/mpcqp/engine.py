@@ -128,7 +128,9 @@ class LinearMpc:
         and runs the interior point only when they fail the KKT check.  For callers that
         solve the same robots tick after tick; results do not depend on it.  ``capacity`` =
         robots remembered (robot indices 0 .. capacity - 1), 0 disables.  Returns the
-        engine-owned device memory (uint8 [capacity, WARM_BYTES]); zero it to forget."""
+        engine-owned device memory (uint8 [capacity, WARM_BYTES]); zero it to forget.
+        Replacing it releases the previous memory to torch's allocator on the current
+        stream: call it between solves issued on that stream."""
         cap = int(capacity)
         if cap < 0:
             raise ValueError("capacity must be >= 0")
