@@ -50,6 +50,10 @@ static_assert(MPCQP_WARM_BYTES == 4 * kMaxN, "warm-start memory: one byte per (s
 #ifndef MPCQP_SPLIT_CHOICE
 #define MPCQP_SPLIT_CHOICE 1   // class 64: wave 1 chooses the next rows, wave 0 reads them; 0: both choose
 #endif
+#ifndef MPCQP_SPLIT96
+#define MPCQP_SPLIT96 1   // class 96: wave 1 chooses, the other five waves read its published choice (+1.2 %)
+#endif
+
 #ifndef MPCQP_PAIR_MAX_NV
 #define MPCQP_PAIR_MAX_NV 96   // pair steps in classes 64 and 96 (class 128: no VGPRs to spare)
 #endif

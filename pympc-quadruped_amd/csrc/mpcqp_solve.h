@@ -615,11 +615,14 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, thr = 0.0, sp = 0.0, up = 0.0;
   // the next rows p (and its pair candidate p2): the most violated row in the dual metric
   // (f32-rounded keys, lowest lane on ties), then the best row of any other foot-step;
-  // with the split choice (class 64) wave 1 publishes {p, p2} in one pass-tagged LDS word
-  constexpr bool kSplit = MPCQP_SPLIT_CHOICE && NV == 64 && C::NW == 2;
+  // with the split choice (classes 64 and 96) wave 1 publishes {p, p2} in one pass-tagged
+  // LDS word the other waves read (class 96: its six waves sit 2-2-1-1 on the SIMDs, so
+  // five fewer argmins free the shared SIMDs' issue: config 4 +1.2 %, bitwise identical)
+  // (class 128 would spill: 138 VGPRs with the split choice)
+  constexpr bool kSplit = MPCQP_SPLIT_CHOICE && ((NV == 64 && C::NW == 2) || (NV == 96 && MPCQP_SPLIT96));
   // early choice: the choosing wave (wave 1 of the split choice; the only wave of the one-wave
   // class 64) chooses the next rows before a pass's rank updates, which then overlap it
-  constexpr bool kEarly = (kSplit || (NV == 64 && C::NW == 1)) && MPCQP_EARLY_CHOICE;
+  constexpr bool kEarly = NV == 64 && (kSplit || C::NW == 1) && MPCQP_EARLY_CHOICE;
   constexpr int kChooser = C::NW == 1 ? 0 : 1;
   auto choose = [&](int tag_it, int& pc, int& pc2) {
     pc = -1;
