@@ -58,7 +58,8 @@ static_assert(MPCQP_WARM_BYTES == 4 * kMaxN, "warm-start memory: one byte per (s
 #define MPCQP_PAIR_MAX_NV 96   // pair steps in classes 64 and 96 (class 128: no VGPRs to spare)
 #endif
 #ifndef MPCQP_CURKEY_MAX_NV
-#define MPCQP_CURKEY_MAX_NV 64   // row choice in the current projected metric up to this class
+#define MPCQP_CURKEY_MAX_NV 96   // row choice in the current projected metric up to this class (DESIGN 4.1;
+                                 // class 96 since its early choice: config 4 +1.5 %)
 #endif
 #ifndef MPCQP_C64_ONEWAVE
 // 1: class 64 as ONE wave per robot (4 x 16 register tiles, 512-VGPR budget: one robot per

@@ -542,8 +542,9 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   // the cone apex.
   int cz[CPL], crt[CPL];
   double s[CPL];
-  // classes 96 / 128 keep the initial metric: their launches are throughput-bound and
-  // the per-pass updates cost more than the passes they save (configs 4 / 5: -3 / -1 %)
+  // class 128 keeps the initial metric: the per-pass updates cost more than the passes they
+  // save (config 5 -1 %); class 96 uses the current one since its choosing wave updates q_c
+  // in the early-choice block (config 4 +1.5 %; before the early choice -3 %)
   constexpr bool kCurKey = NV <= MPCQP_CURKEY_MAX_NV;
   float qm[CPL];   // a_c^T P a_c (f32; classes 96 / 128: 1 / sqrt(a_c^T W a_c)): scales the f32 row key
   auto cdot = [&](const double* v, int k) -> double {
