@@ -672,11 +672,18 @@ def main():
         if traffic_note:
             line["roofline"]["traffic_note"] = traffic_note
         if n_ipm:
-            line["roofline"]["note"] = (
-                f"{n_ipm} of {nbat * Bpg} robots have n > 128 (the interior-point class): they are priced at "
-                "the reference's dense formulation + one n^3/3 factorisation, work that class never executes "
-                "(it solves the uncondensed horizon by Riccati recursions), so frac / executed_frac of this "
-                "line are reference-work rates, not hardware utilisation")
+            # robots of the interior-point class would be priced at the reference's dense
+            # formulation + one n^3/3 factorisation, work that class never executes (it solves
+            # the uncondensed horizon by Riccati recursions): no roofline fraction for such a
+            # line, the rate goes to a field of its own
+            rf = line["roofline"]
+            line["reference_work_rate"] = {
+                "achieved": rf["achieved"], "unit": "TFLOP/s", "vs_fp64_peak": rf["frac"],
+                "note": (f"{n_ipm} of {nbat * Bpg} robots have n > 128 (the interior-point class); the whole "
+                         "batch is priced at the reference's condensed-dense work (SURVEY §8(d)), which that "
+                         "class does not execute: a reference-work rate, not hardware utilisation")}
+            rf["achieved"] = rf["frac"] = rf["executed_frac"] = None
+            rf["note"] = "frac null: the line's interior-point robots execute none of the priced work (reference_work_rate)"
         if no_hint is not None:
             line["no_hint"] = no_hint
         if two_streams is not None:

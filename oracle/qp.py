@@ -57,6 +57,7 @@ def solve_qp_dual_active_set(H, g, C, lb, ub, max_iter=10000, tol=1e-11):
     u = np.zeros(0)
     it = 0
     scale = 1.0 + np.abs(b).max(initial=0.0)
+    rounding_accept = []   # (row, its multiplier, the largest violation) of a rounding-level stop
     while True:
         s = A @ x - b
         p = int(np.argmin(s)) if len(s) else -1
@@ -93,9 +94,13 @@ def solve_qp_dual_active_set(H, g, C, lb, ub, max_iter=10000, tol=1e-11):
                 # arithmetic that is infeasibility, which the MPC QP cannot have (U = 0 is
                 # feasible); a violation at rounding level (a flight schedule's forced-zero
                 # GRFs at N = 32: s = -3e-11 against dn = 4e4) is rounding noise of the
-                # J / R updates, and p is the most violated row, so every row is satisfied
-                # to that level.
-                if s[p] >= -1e-8 * scale:
+                # J / R updates.  Accepted only when EVERY row, re-evaluated at the current x
+                # (earlier partial steps for p have moved it), is satisfied to 1e-8 * scale;
+                # p then keeps the multiplier u_p its partial steps gave it (stationarity
+                # H x + g = A^T u + u_p a_p holds throughout), reported in y and in info.
+                s_now = A @ x - b
+                if (-s_now).max(initial=0.0) <= 1e-8 * scale:
+                    rounding_accept.append((p, u_p, float(-s_now.min(initial=0.0))))
                     done = True
                     break
                 raise RuntimeError("QP infeasible (cannot happen for the MPC QP)")
@@ -120,7 +125,10 @@ def solve_qp_dual_active_set(H, g, C, lb, ub, max_iter=10000, tol=1e-11):
     y = np.zeros(np.asarray(C).shape[0])
     for k, j in enumerate(active):
         y[src[j]] += sgn[j] * u[k]
-    return x, y, dict(iterations=it, active=[(int(src[j]), int(sgn[j])) for j in active])
+    for j, up, _ in rounding_accept:
+        y[src[j]] += sgn[j] * up
+    return x, y, dict(iterations=it, active=[(int(src[j]), int(sgn[j])) for j in active],
+                      rounding_accept=[(int(src[j]), float(up), v) for j, up, v in rounding_accept])
 
 
 def _add(R, J, d, q):

@@ -61,19 +61,11 @@ static_assert(MPCQP_WARM_BYTES == 4 * kMaxN, "warm-start memory: one byte per (s
 #define MPCQP_CURKEY_MAX_NV 96   // row choice in the current projected metric up to this class (DESIGN 4.1;
                                  // class 96 since its early choice: config 4 +1.5 %)
 #endif
-#ifndef MPCQP_C64_ONEWAVE
-// 1: class 64 as ONE wave per robot (4 x 16 register tiles, 512-VGPR budget: one robot per
-// SIMD, four per CU) -- no workgroup barrier in the sweep or the active-set loop
-#define MPCQP_C64_ONEWAVE 0
+#ifndef MPCQP_PRIO_T
+#define MPCQP_PRIO_T 0   // A/B only: class 64 raises its waves' issue priority after T, 2T, 3T iterations
 #endif
-#ifndef MPCQP_C96_TW
-// class 96's register tile width: 6 (4 x 6 tiles, 6 waves, two waves share two of the four
-// SIMDs) or 12 (4 x 12 tiles, 3 waves, one per SIMD with the 512-VGPR budget)
-#define MPCQP_C96_TW 6
-#endif
-#ifndef MPCQP_C128_TW
-// class 128's register tile width: 8 (8 waves, two per SIMD) or 16 (4 waves, one per SIMD)
-#define MPCQP_C128_TW 8
+#ifndef MPCQP_PRIO_V
+#define MPCQP_PRIO_V 0   // A/B only: class 64's issue priority from its start's violated-row count (>= V, V + 4, V + 8)
 #endif
 #ifndef MPCQP_ASM_COMBO
 // class 64's z / r column combination as one computed jump (mpcqp_combo_asm.h) instead of
@@ -365,14 +357,25 @@ __device__ __forceinline__ int xcd_robot(int bid, int B) {
 
 // class 64's capacity (stance variables)
 constexpr int kCap64 = 64;
-// interior-point class: global S_k slots per CU (at most three robots fit a CU's LDS)
+// interior-point class: global S_k slots per CU.  Every layout takes more than a fifth of a
+// CU's LDS, so at most kIpmPerCU of its (one-wave) workgroups are resident on a CU at once
+// and a claim finds a free slot without waiting (ipm_claim_slot).
 constexpr int kIpmPerCU = 4;
+template <int NM, bool FULL, bool MG>
+constexpr bool ipm_within_slots() {
+  return sizeof(IpmSharedT<NM, FULL, MG>) > 160 * 1024 / (kIpmPerCU + 1);
+}
+static_assert(ipm_within_slots<16, false, true>() && ipm_within_slots<16, true, true>() &&
+                  ipm_within_slots<16, false, false>() && ipm_within_slots<16, true, false>() &&
+                  ipm_within_slots<kDenseN, false, false>() && ipm_within_slots<kDenseN, true, false>() &&
+                  ipm_within_slots<kMaxN, false, false>() && ipm_within_slots<kMaxN, true, false>(),
+              "an interior-point layout fits more workgroups on a CU than kIpmPerCU slots");
 
 // Class NV = 64: one 2-wave workgroup per robot of the batch.  Robots with more
 // than 64 stance variables are appended to `queue` (when given) for class 96, those
 // with more than 96 to `queue_big` (when given) for class 128.
 template <bool FULL>
-__global__ __launch_bounds__(Cfg<64>::NT) __attribute__((amdgpu_waves_per_eu(MPCQP_C64_ONEWAVE ? 1 : 2, Cfg<64>::NW))) void mpcqp_kernel_64(
+__global__ __launch_bounds__(Cfg<64>::NT) __attribute__((amdgpu_waves_per_eu(2, Cfg<64>::NW))) void mpcqp_kernel_64(
     KParams P, int B, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
@@ -421,12 +424,7 @@ __global__ __launch_bounds__(Cfg<96>::NT) __attribute__((amdgpu_waves_per_eu((Cf
 // workgroups, queue[4..] = robot indices).  Workloads that fit class 64 skip this
 // launch via mpcqp_set_stance_hint.
 template <bool FULL>
-#if MPCQP_C128_TW == 16
-#define MPCQP_C128_ATTR __attribute__((amdgpu_waves_per_eu(1, 1)))
-#else
-#define MPCQP_C128_ATTR
-#endif
-__global__ __launch_bounds__(Cfg<128>::NT) MPCQP_C128_ATTR void mpcqp_kernel_128(
+__global__ __launch_bounds__(Cfg<128>::NT) void mpcqp_kernel_128(
     KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
@@ -454,11 +452,14 @@ __global__ __launch_bounds__(Cfg<128>::NT) MPCQP_C128_ATTR void mpcqp_kernel_128
 // Riccati-factored interior point + active-set polish (mpcqp_ipm.h).  Same launch / reset
 // protocol as class 128.  FULL: non-diagonal weights (mpcqp_set_weights).
 // A free slot of the interior-point class's global S_k scratch: one bit per slot in `bits`
-// (nw words), claimed with atomicOr, released with atomicAnd.  More slots than robots can
-// be resident at once (LDS-bound: <= 3 per CU; kIpmPerCU = 4 slots per CU), so the search
-// always finds one.  Called by one lane.
+// (nw words), claimed with atomicOr, released with atomicAnd.  The search terminates: a slot
+// holder never waits for anything before it releases its slot, and there are at least as
+// many slots as workgroups of the class can be resident at once (kIpmPerCU per CU, every
+// layout LDS-bound to at most that: the static_assert above), so a free one exists whenever
+// a workgroup searches.  Called by one lane.
 __device__ __forceinline__ int ipm_claim_slot(unsigned* bits, int nw, int start) {
   for (int i = 0;; ++i) {
+    if (i >= nw) __builtin_amdgcn_s_sleep(2);   // a full sweep found none: back off (never expected)
     const int w = (start + i) % nw;
     unsigned m = ~__hip_atomic_load(&bits[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     while (m) {
@@ -490,7 +491,7 @@ __global__ __launch_bounds__(LANES) void mpcqp_kernel_ipm(
   int slot = 0;
   if (tid == 0) slot = ipm_claim_slot(sbits, nsw, k % nsw);
   slot = __builtin_amdgcn_readlane(slot, 0);
-  solve_robot_ipm<FULL, NM, MG>(P, b, sm, sscratch + (size_t)slot * IPM_S_SLOT, x0g, xrefg, contactg, feetg, robotg, u0g,
+  solve_robot_ipm<FULL, NM, MG>(P, b, sm, sscratch + (size_t)slot * IpmSlot<NM>::SIZE, x0g, xrefg, contactg, feetg, robotg, u0g,
                             Ug, statusg, itersg);
   if (tid == 0) {
     atomicAnd(&sbits[slot >> 5], ~(1u << (slot & 31)));   // the solve's S_k reads are done
@@ -518,8 +519,6 @@ struct QueueSet {
   // (routing) class and joined back at the end of the call (created on first use)
   hipStream_t side;
   hipEvent_t ev_fork, ev_join;
-  double* sscratch;   // the interior-point class's Riccati S_k, one slot per workgroup (first use)
-  int sslots;
   hipEvent_t ev_done;   // recorded on `stream` after each call's last launch (eviction waits on it)
 };
 
@@ -531,9 +530,6 @@ static void release_set(QueueSet& q) {
   if (q.ev_done) (void)hipEventDestroy(q.ev_done);
   q.ev_done = nullptr;
   if (q.side) (void)hipStreamDestroy(q.side);
-  if (q.sscratch) (void)hipFree(q.sscratch);
-  q.sscratch = nullptr;
-  q.sslots = 0;
   q.buf = nullptr;
   q.ev_fork = q.ev_join = nullptr;
   q.side = nullptr;
@@ -547,6 +543,12 @@ struct mpcqp_ctx {
   int ncu;
   std::vector<QueueSet> queues;
   unsigned long long use_clock;
+  // the interior-point class's global slots (Riccati S_k; at N <= 16 also M_k, M_k^T and the
+  // saved iterate): kIpmPerCU per CU, one pool for every stream of the context (the slots in
+  // use never exceed the class's resident workgroups, whichever launches they belong to),
+  // ipm_slot_doubles(horizon) each, then the slot bitmap; allocated on first use
+  double* sscratch;
+  int sslots;
   double* wdev;       // full Q (13 x 13) then R (12 x 12) on the device (mpcqp_set_weights); nullptr: diagonal
   double q_full[13 * 13];   // the current weights as whole matrices (host copies: a NULL argument
   double r_full[12 * 12];   // of mpcqp_set_weights keeps that matrix, off-diagonal entries included)
@@ -601,24 +603,27 @@ static QueueSet* stream_queues(mpcqp_ctx* ctx, hipStream_t st, int batch, int* e
     QueueSet* lru = &ctx->queues[0];
     for (auto& q : ctx->queues)
       if (q.used < lru->used) lru = &q;
-    if (lru->ev_done && hipEventSynchronize(lru->ev_done) != hipSuccess) {
-      *err = set_err(ctx, MPCQP_ERR_HIP, "queue eviction: event sync failed");
+    // ev_done is recorded after every call that launched anything on the set, on its error
+    // paths too; without one, wait for the whole device
+    const hipError_t se = lru->ev_done ? hipEventSynchronize(lru->ev_done) : hipDeviceSynchronize();
+    if (se != hipSuccess) {
+      *err = set_err(ctx, MPCQP_ERR_HIP, "queue eviction: sync failed");
       return nullptr;
     }
     // every launch that used the set is done: its queues are back at rest (each kernel
-    // resets its header) and its S_k slots free -- the new stream reuses them as they are
+    // resets its header) -- the new stream reuses them as they are
     lru->stream = st;
     lru->used = ++ctx->use_clock;
     qs = lru;
   }
   if (!qs) {
-    ctx->queues.push_back(QueueSet{st, 0, nullptr, ++ctx->use_clock, nullptr, nullptr, nullptr, nullptr, 0, nullptr});
-    qs = &ctx->queues.back();
-    if (hipEventCreateWithFlags(&qs->ev_done, hipEventDisableTiming) != hipSuccess) {
-      qs->ev_done = nullptr;
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
       *err = set_err(ctx, MPCQP_ERR_HIP, "queue event creation failed");
       return nullptr;
     }
+    ctx->queues.push_back(QueueSet{st, 0, nullptr, ++ctx->use_clock, nullptr, nullptr, nullptr, ev});
+    qs = &ctx->queues.back();
   }
   if (qs->buf) {
     if (hipStreamSynchronize(st) != hipSuccess) {
@@ -691,6 +696,8 @@ int mpcqp_create(const mpcqp_params* p, int32_t device, mpcqp_ctx** out) {
   ctx->stance_min = 0;
   ctx->ncu = 0;
   ctx->use_clock = 0;
+  ctx->sscratch = nullptr;
+  ctx->sslots = 0;
   ctx->wdev = nullptr;
   ctx->warm = nullptr;
   ctx->warm_cap = 0;
@@ -781,20 +788,22 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
     if (!qs) return qerr;
     q = qs->buf;
   }
-  if (giant && !qs->sscratch) {   // the interior-point class's global S_k slots (first use)
+  const size_t sstride = (size_t)ipm_slot_doubles(kp.N);   // doubles per slot
+  if (giant && !ctx->sscratch) {   // the interior-point class's global slots (first use)
     const int slots = 32 * ((kIpmPerCU * ctx->ncu + 31) / 32);
-    const size_t sbytes = sizeof(double) * IPM_S_SLOT * (size_t)slots;
-    if (hipMalloc(&qs->sscratch, sbytes + slots / 8) != hipSuccess) {
-      qs->sscratch = nullptr;
+    const size_t sbytes = sizeof(double) * sstride * (size_t)slots;
+    if (hipMalloc(&ctx->sscratch, sbytes + slots / 8) != hipSuccess) {
+      ctx->sscratch = nullptr;
       return set_err(ctx, MPCQP_ERR_ALLOC, "interior-point scratch allocation failed");
     }
-    // the slot bitmap after the slots: all free (every solve releases its slot)
-    if (hipMemsetAsync((char*)qs->sscratch + sbytes, 0, slots / 8, st) != hipSuccess) {
-      (void)hipFree(qs->sscratch);
-      qs->sscratch = nullptr;
+    // the slot bitmap after the slots: all free (every solve releases its slot); synchronous,
+    // so a launch on any stream of the context finds it cleared
+    if (hipMemset((char*)ctx->sscratch + sbytes, 0, slots / 8) != hipSuccess) {
+      (void)hipFree(ctx->sscratch);
+      ctx->sscratch = nullptr;
       return set_err(ctx, MPCQP_ERR_HIP, "interior-point scratch init failed");
     }
-    qs->sslots = slots;
+    ctx->sslots = slots;
   }
   // the interior-point class (one wave per robot, latency-bound) on a side stream as soon
   // as the first class has routed its robots, beside classes 96 / 128 instead of behind
@@ -814,10 +823,10 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
                 : kp.N <= kDenseN ? (full ? mpcqp_kernel_ipm<true, kDenseN> : mpcqp_kernel_ipm<false, kDenseN>)
                                   : (full ? mpcqp_kernel_ipm<true, kMaxN> : mpcqp_kernel_ipm<false, kMaxN>);
     // one workgroup per robot of the batch (the queued ones beyond the count exit at once)
-    unsigned* sbits = (unsigned*)(qs->sscratch + (size_t)IPM_S_SLOT * qs->sslots);
+    unsigned* sbits = (unsigned*)(ctx->sscratch + sstride * ctx->sslots);
     hipLaunchKernelGGL(kern, dim3(batch), dim3(LANES), 0, s, kp, x0, xref, contact, feet, robot, u0, U,
                        (int*)status, (int*)iters, q + 2 * (4 + (size_t)cap), first == 3 ? (int)batch : 0,
-                       qs->sscratch, sbits, qs->sslots / 32);
+                       ctx->sscratch, sbits, ctx->sslots / 32);
     ipm_done = true;
     return hipGetLastError();
   };
@@ -836,32 +845,38 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   int* q3 = giant ? q + 2 * qstride : nullptr;
   hipError_t e = hipSuccess;
   int fe = MPCQP_OK;
+  // an error after a launch still marks the queue set's last use: eviction waits on ev_done
+  auto failed = [&](int code) -> int {
+    if (fork && ipm_done) (void)hipStreamWaitEvent(st, qs->ev_join, 0);   // the side stream's launch too
+    if (qs) (void)hipEventRecord(qs->ev_done, st);
+    return code;
+  };
   if (first == 0) {
     hipLaunchKernelGGL(full ? mpcqp_kernel_64<true> : mpcqp_kernel_64<false>, dim3(batch), dim3(Cfg<64>::NT), 0, st, kp, (int)batch, x0, xref, contact,
                        feet, robot, u0, U, (int*)status, (int*)iters, q1, q2, q3);
     e = hipGetLastError();
-    if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch: ") + hipGetErrorString(e));
-    if ((fe = fork_ipm()) != MPCQP_OK) return fe;
+    if (e != hipSuccess) return failed(set_err(ctx, MPCQP_ERR_HIP, std::string("launch: ") + hipGetErrorString(e)));
+    if ((fe = fork_ipm()) != MPCQP_OK) return failed(fe);
   }
   if (large && first <= 1) {
     hipLaunchKernelGGL(full ? mpcqp_kernel_96<true> : mpcqp_kernel_96<false>, dim3(batch), dim3(Cfg<96>::NT), 0, st, kp, x0, xref, contact, feet, robot,
                        u0, U, (int*)status, (int*)iters, q1, q2, q3, first == 1 ? (int)batch : 0);
     e = hipGetLastError();
-    if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (96): ") + hipGetErrorString(e));
-    if ((fe = fork_ipm()) != MPCQP_OK) return fe;
+    if (e != hipSuccess) return failed(set_err(ctx, MPCQP_ERR_HIP, std::string("launch (96): ") + hipGetErrorString(e)));
+    if ((fe = fork_ipm()) != MPCQP_OK) return failed(fe);
   }
   if (huge && first <= 2) {
     hipLaunchKernelGGL(full ? mpcqp_kernel_128<true> : mpcqp_kernel_128<false>, dim3(batch), dim3(Cfg<128>::NT), 0, st, kp, x0, xref, contact, feet, robot,
                        u0, U, (int*)status, (int*)iters, q2, q3, first == 2 ? (int)batch : 0);
     e = hipGetLastError();
-    if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (128): ") + hipGetErrorString(e));
-    if ((fe = fork_ipm()) != MPCQP_OK) return fe;
+    if (e != hipSuccess) return failed(set_err(ctx, MPCQP_ERR_HIP, std::string("launch (128): ") + hipGetErrorString(e)));
+    if ((fe = fork_ipm()) != MPCQP_OK) return failed(fe);
   }
   if (giant && !ipm_done) {   // the interior-point class takes the batch directly (or no side stream)
     e = launch_ipm(st);
-    if (e != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, std::string("launch (ipm): ") + hipGetErrorString(e));
+    if (e != hipSuccess) return failed(set_err(ctx, MPCQP_ERR_HIP, std::string("launch (ipm): ") + hipGetErrorString(e)));
   } else if (fork && hipStreamWaitEvent(st, qs->ev_join, 0) != hipSuccess) {
-    return set_err(ctx, MPCQP_ERR_HIP, "interior-point join failed");
+    return failed(set_err(ctx, MPCQP_ERR_HIP, "interior-point join failed"));
   }
   if (qs && hipEventRecord(qs->ev_done, st) != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, "queue event record failed");
   return MPCQP_OK;
@@ -1018,6 +1033,7 @@ int mpcqp_destroy(mpcqp_ctx* ctx) {
     // hipFree synchronises the device before releasing the memory: no per-stream sync
     // (a recorded stream may already have been destroyed by the caller)
     for (auto& q : ctx->queues) release_set(q);
+    if (ctx->sscratch) (void)hipFree(ctx->sscratch);
     if (ctx->wdev) (void)hipFree(ctx->wdev);
     for (double* o : ctx->retired) (void)hipFree(o);
   }

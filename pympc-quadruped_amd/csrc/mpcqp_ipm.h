@@ -138,9 +138,18 @@ struct alignas(16) IpmSharedT {
 static_assert(sizeof(IpmSharedT<16, false, true>) <= 160 * 1024 / 4, "N <= 16, diagonal weights: four robots per CU");
 static_assert(sizeof(IpmSharedT<16, true, true>) <= 160 * 1024 / 3, "N <= 16, full weights: three robots per CU");
 static_assert(sizeof(IpmSharedT<16, true, false>) <= 160 * 1024 / 3, "N <= 16, M_k in LDS: three robots per CU");
-// one robot's global slot: S_k, then (NM <= 16) M_k, M_k^T and the saved iterate
-constexpr int IPM_SLOT_S = 0, IPM_SLOT_M = kMaxN * 144, IPM_SLOT_MT = 2 * kMaxN * 144, IPM_SLOT_US = 3 * kMaxN * 144;
-constexpr int IPM_S_SLOT = 3 * kMaxN * 144 + kMaxN * NU;   // doubles per slot
+// One robot's global slot (doubles): S_k, then -- used by the four-per-CU layout at NM = 16
+// only -- M_k, M_k^T and the saved iterate.  The stride depends on the stage count alone, so
+// one pool per context (sized for its horizon) serves both N <= 16 layouts.
+template <int NM>
+struct IpmSlot {
+  static constexpr int M = NM * 144, MT = 2 * NM * 144, US = 3 * NM * 144;
+  static constexpr int SIZE = NM <= 16 ? 3 * NM * 144 + NM * NU : NM * 144;
+};
+// the slot stride of the layouts a context of horizon N launches (host and device)
+__host__ __device__ constexpr int ipm_slot_doubles(int N) {
+  return N <= 16 ? IpmSlot<16>::SIZE : N <= kDenseN ? IpmSlot<kDenseN>::SIZE : IpmSlot<kMaxN>::SIZE;
+}
 
 // 12 consecutive doubles of a 16-B aligned LDS vector, 16 B per read
 __device__ __forceinline__ void ld12(double (&v)[12], const double* p) {
@@ -507,8 +516,8 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       const int r = lr + 4 * i;
       if (r < 12 && lc < 12) {
         if constexpr (kMG) {
-          Sg[IPM_SLOT_M + k * 144 + 12 * r + lc] = Mr[i];
-          Sg[IPM_SLOT_MT + k * 144 + 12 * lc + r] = Mr[i];
+          Sg[IpmSlot<NM>::M + k * 144 + 12 * r + lc] = Mr[i];
+          Sg[IpmSlot<NM>::MT + k * 144 + 12 * lc + r] = Mr[i];
         } else {
           sm.mk.M[k][12 * r + lc] = Mr[i];
         }
@@ -665,14 +674,14 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     double p = 0.0;
     if constexpr (kMG) {   // row l12 of M_k from the global slot, the next stage's issued ahead
       double mn[12];
-      if (N > 1) ld12g(mn, Sg + IPM_SLOT_M + (N - 1) * 144 + 12 * l12);
+      if (N > 1) ld12g(mn, Sg + IpmSlot<NM>::M + (N - 1) * 144 + 12 * l12);
       for (int k = N - 1; k >= 0; --k) {
         if (lane < NU) sm.ph[k][lane] = p;
         if (k > 0) {
           double mr[12], r[12];
 #pragma unroll
           for (int j = 0; j < 12; ++j) mr[j] = mn[j];
-          if (k > 1) ld12g(mn, Sg + IPM_SLOT_M + (k - 1) * 144 + 12 * l12);
+          if (k > 1) ld12g(mn, Sg + IpmSlot<NM>::M + (k - 1) * 144 + 12 * l12);
           const double ck = sm.lc[k][l12];
 #pragma unroll
           for (int j = 0; j < 12; ++j) r[j] = readlane_d(p, j);
@@ -714,14 +723,14 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     double dx = 0.0;
     if constexpr (kMG) {   // column l12 of M_k = row l12 of the stored transpose, issued ahead
       double mn[12];
-      if (N > 1) ld12g(mn, Sg + IPM_SLOT_MT + 12 * l12);
+      if (N > 1) ld12g(mn, Sg + IpmSlot<NM>::MT + 12 * l12);
       for (int k = 0; k < N; ++k) {
         if (lane < NU) sm.dxh[k][lane] = dx;
         if (k < N - 1) {
           double mc[12], r[12];
 #pragma unroll
           for (int j = 0; j < 12; ++j) mc[j] = mn[j];
-          if (k < N - 2) ld12g(mn, Sg + IPM_SLOT_MT + (k + 1) * 144 + 12 * l12);
+          if (k < N - 2) ld12g(mn, Sg + IpmSlot<NM>::MT + (k + 1) * 144 + 12 * l12);
           const double ek = sm.lc[k][l12];
 #pragma unroll
           for (int j = 0; j < 12; ++j) r[j] = readlane_d(dx, j);
@@ -994,7 +1003,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       }
       // U is overwritten by the polish: keep the IPM iterate
       for (int e = lane; e < N * NU; e += NT) {
-        if constexpr (kMG) Sg[IPM_SLOT_US + e] = sm.U[e / NU][e % NU];
+        if constexpr (kMG) Sg[IpmSlot<NM>::US + e] = sm.U[e / NU][e % NU];
         else sm.us.Us[e / NU][e % NU] = sm.U[e / NU][e % NU];
       }
       fsync<NT>();
@@ -1004,7 +1013,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
         break;
       }
       for (int e = lane; e < N * NU; e += NT) {
-        if constexpr (kMG) sm.U[e / NU][e % NU] = Sg[IPM_SLOT_US + e];
+        if constexpr (kMG) sm.U[e / NU][e % NU] = Sg[IpmSlot<NM>::US + e];
         else sm.U[e / NU][e % NU] = sm.us.Us[e / NU][e % NU];
       }
       fsync<NT>();

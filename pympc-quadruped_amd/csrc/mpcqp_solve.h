@@ -28,7 +28,7 @@
 template <int NV>
 struct Cfg {
   // tile width: 4 x TW register tiles
-  static constexpr int TW = NV == 96 ? MPCQP_C96_TW : NV == 128 ? MPCQP_C128_TW : (MPCQP_C64_ONEWAVE ? 16 : 8);
+  static constexpr int TW = NV == 96 ? 6 : 8;
   static constexpr int NW = NV * NV / (4 * TW * LANES);   // waves per robot
   static constexpr int NT = NW * LANES;
   static constexpr int TCN = NV / TW;         // tile columns (lanes per tile row)
@@ -37,7 +37,7 @@ struct Cfg {
   static constexpr int VPL = (NV + LANES - 1) / LANES;   // variables / slots per lane
   static constexpr int VEC = VPL * LANES;     // LDS vector length (entries >= NV are padding)
   static_assert(NW * LANES * 4 * TW == NV * NV, "4 x TW tiles");
-  static_assert(TCN == 4 || TCN == 8 || TCN == 16 || TCN == 32, "tile rows are reduced over 4 to 32 lanes");
+  static_assert(TCN == 8 || TCN == 16, "tile rows are reduced over 8 or 16 lanes");
 };
 
 // Every class keeps a copy of H (its register tiles, lane-interleaved) in LDS for
@@ -96,41 +96,10 @@ __device__ __forceinline__ double dpp_shl1(double v) {
   const int hi = __builtin_amdgcn_update_dpp(0, (int)(bits >> 32), DPP_SHL1, 0xF, 0xF, true);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
-// lane i reads lane i + 1 across the whole wave (wave_shl:1): tile rows of 32 lanes span two
-// 16-lane DPP rows, so a foot-step straddling tile columns 15 | 16 needs the wave shift
-constexpr int DPP_WSHL1 = 0x130;
-__device__ __forceinline__ double dpp_wshl1(double v) {
-  const long long bits = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)bits, DPP_WSHL1, 0xF, 0xF, true);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(bits >> 32), DPP_WSHL1, 0xF, 0xF, true);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
 // Sum 4 row partials over the TCN lanes of a tile row.  Lane keeps row
 // 4tr + 2 bit2(lane) + bit1(lane) (see trow / twriter).
-// lane i <- lane i ^ 16 (ds_swizzle bit mode inside 32 lanes: and 0x1f, xor 0x10)
-__device__ __forceinline__ double swz_xor16(double v) {
-  const long long bits = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_ds_swizzle((int)bits, 0x401F);
-  const int hi = __builtin_amdgcn_ds_swizzle((int)(bits >> 32), 0x401F);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
 template <int TCN>
 __device__ __forceinline__ double tile_reduce(const double (&acc)[4], int lane) {
-  if constexpr (TCN == 4) {   // one-wave class 64 (4 x 16 tiles): lane keeps row 4tr + (lane & 3)
-    const bool hi2 = (lane & 2) != 0;
-    double k2[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const double send = hi2 ? acc[k] : acc[2 + k];
-      const double keep = hi2 ? acc[2 + k] : acc[k];
-      k2[k] = keep + dpp_d<DPP_XOR2>(send);
-    }
-    const bool hi1 = (lane & 1) != 0;
-    const double send = hi1 ? k2[0] : k2[1];
-    const double keep = hi1 ? k2[1] : k2[0];
-    return keep + dpp_d<DPP_XOR1>(send);
-  }
   const bool hi4 = (lane & 4) != 0;
   double k2[2];
 #pragma unroll
@@ -144,17 +113,16 @@ __device__ __forceinline__ double tile_reduce(const double (&acc)[4], int lane) 
   const double keep = hi2 ? k2[1] : k2[0];
   double y = keep + dpp_d<DPP_XOR2>(send);
   y += dpp_d<DPP_XOR1>(y);
-  if constexpr (TCN >= 16) y += dpp_d<DPP_ROR8>(y);
-  if constexpr (TCN == 32) y += swz_xor16(y);
+  if constexpr (TCN == 16) y += dpp_d<DPP_ROR8>(y);
   return y;
 }
 template <int TCN>
 __device__ __forceinline__ int trow(int tr, int lane) {
-  return TCN == 4 ? 4 * tr + (lane & 3) : 4 * tr + 2 * ((lane >> 2) & 1) + ((lane >> 1) & 1);
+  return 4 * tr + 2 * ((lane >> 2) & 1) + ((lane >> 1) & 1);
 }
 template <int TCN>
 __device__ __forceinline__ bool twriter(int lane) {
-  return TCN == 4 ? true : TCN == 32 ? (lane & 25) == 0 : TCN == 16 ? (lane & 9) == 0 : (lane & 1) == 0;
+  return TCN == 16 ? (lane & 9) == 0 : (lane & 1) == 0;
 }
 
 // y = M v, v in LDS; returns row trow<TCN>(tr, lane)'s value
@@ -546,7 +514,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   // save (config 5 -1 %); class 96 uses the current one since its choosing wave updates q_c
   // in the early-choice block (config 4 +1.5 %; before the early choice -3 %)
   constexpr bool kCurKey = NV <= MPCQP_CURKEY_MAX_NV;
-  float qm[CPL];   // a_c^T P a_c (f32; classes 96 / 128: 1 / sqrt(a_c^T W a_c)): scales the f32 row key
+  float qm[CPL];   // a_c^T P a_c (f32, classes 64 / 96; class 128: 1 / sqrt(a_c^T W a_c)): scales the f32 row key
   auto cdot = [&](const double* v, int k) -> double {
     const double* a = sm.mt.rows[crt[k]];
     const double* vf = v + cz[k];
@@ -578,6 +546,19 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     u[k] = 0.0;
   }
   if (tid == 0) sm.choice = 0;   // no pass tag yet (MPCQP_SPLIT_CHOICE)
+#if MPCQP_PRIO_V > 0
+  // A/B: a robot whose start violates many rows (a predictor of a long active set, corr 0.78
+  // with the iteration count on config 2) takes issue priority over its SIMD partners
+  if constexpr (NV == 64) {
+    int nv = 0;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) nv += __popcll(__ballot(s[k] < -1e-9));
+    nv = uni(nv);
+    if (nv >= MPCQP_PRIO_V + 8) __builtin_amdgcn_s_setprio(3);
+    else if (nv >= MPCQP_PRIO_V + 4) __builtin_amdgcn_s_setprio(2);
+    else if (nv >= MPCQP_PRIO_V) __builtin_amdgcn_s_setprio(1);
+  }
+#endif
   // the cone rows' coefficients (lanes 0..17: row r's a_i at 3 r + i) and dependency
   // thresholds 1e-12 |a_r|^2 wscale (lanes 18..23) in one register, read by v_readlane into
   // SGPRs when a row is chosen (an LDS load + readfirstlane chain otherwise)
@@ -624,8 +605,8 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   // early choice: the choosing wave (wave 1 of the split choice; the only wave of the one-wave
   // class 64) chooses the next rows before a pass's rank updates, which then overlap it
   // (class 96 with the split choice: config 4 +4.7 %, bitwise identical)
-  constexpr bool kEarly = (NV == 64 || NV == 96) && (kSplit || C::NW == 1) && MPCQP_EARLY_CHOICE;
-  constexpr int kChooser = C::NW == 1 ? 0 : 1;
+  constexpr bool kEarly = (NV == 64 || NV == 96) && kSplit && MPCQP_EARLY_CHOICE;
+  constexpr int kChooser = 1;
   auto choose = [&](int tag_it, int& pc, int& pc2) {
     pc = -1;
     pc2 = -1;
@@ -709,6 +690,9 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   };
+#if MPCQP_PRIO_T > 0
+  int prio_ = 0;
+#endif
   bool early = false;   // kEarly: wave 1 already holds (and has published) the next choice
   int epc = -1, epc2 = -1;
   SEC(0);
@@ -796,6 +780,15 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       status = MPCQP_STATUS_MAX_ITER;
       break;
     }
+#if MPCQP_PRIO_T > 0
+    // a robot still iterating past T, 2T, 3T iterations takes issue priority over the
+    // younger-in-iterations robots sharing its SIMDs (the launch is its slowest robot)
+    if constexpr (NV == 64) {
+      if (it >= MPCQP_PRIO_T && prio_ < 1) { __builtin_amdgcn_s_setprio(1); prio_ = 1; }
+      if (it >= 2 * MPCQP_PRIO_T && prio_ < 2) { __builtin_amdgcn_s_setprio(2); prio_ = 2; }
+      if (it >= 3 * MPCQP_PRIO_T && prio_ < 3) { __builtin_amdgcn_s_setprio(3); prio_ = 3; }
+    }
+#endif
     SEC(1);
     // z = P a_p, r = R a_p: rows 4tr..4tr+3 in the lanes of tile column tcA
     // (R rows of slots no wave member holds active are zero: skipped)
@@ -805,28 +798,10 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     constexpr bool kAsmCombo = (NV == 64 || NV == 128) && TW == 8 && MPCQP_ASM_COMBO;
     auto combo_store = [&](int cA, int tA, double e0, double e1, double e2, double* dz, double* dr) {
       double zq[4], rq[4];
-      if constexpr (TW % 3 == 0) {   // foot-steps start at a register column 3k: never straddle,
+      if constexpr (TW == 6) {   // foot-steps start at register column 0 or 3: never straddle,
         // so the uniform (SGPR) coefficients need no per-lane mask: only tile column tA stores
-        if constexpr (TW == 3) {   // one foot-step per tile column
-          colcombo_u<0, TW>(W, Rm, e0, e1, e2, rlive, zq, rq);
-        } else if constexpr (TW == 6) {
-          if (cA == 0) colcombo_u<0, TW>(W, Rm, e0, e1, e2, rlive, zq, rq);
-          else colcombo_u<3, TW>(W, Rm, e0, e1, e2, rlive, zq, rq);
-        } else {   // TW = 12
-          switch (cA) {
-            case 0: colcombo_u<0, TW>(W, Rm, e0, e1, e2, rlive, zq, rq); break;
-            case 3: colcombo_u<3, TW>(W, Rm, e0, e1, e2, rlive, zq, rq); break;
-            case 6: colcombo_u<6, TW>(W, Rm, e0, e1, e2, rlive, zq, rq); break;
-            default: colcombo_u<9, TW>(W, Rm, e0, e1, e2, rlive, zq, rq); break;
-          }
-        }
-      } else if constexpr (TW == 4) {
-        switch (cA) {
-          case 0: colcombo<0, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-          case 1: colcombo<1, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-          case 2: colcombo<2, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-          default: colcombo<3, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-        }
+        if (cA == 0) colcombo_u<0, TW>(W, Rm, e0, e1, e2, rlive, zq, rq);
+        else colcombo_u<3, TW>(W, Rm, e0, e1, e2, rlive, zq, rq);
       } else if constexpr (kAsmCombo) {
         // one computed jump into straight-line cases (mpcqp_combo_asm.h); R's half
         // unconditionally (rows of no active slot are zero; a second, P-only table for those
@@ -854,28 +829,14 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
           case 4: colcombo<4, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
           case 5: colcombo<5, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
           case 6: colcombo<6, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-          case 7: colcombo<7, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-          default:
-            if constexpr (TW == 16) {
-              switch (cA) {
-                case 8: colcombo<8, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-                case 9: colcombo<9, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-                case 10: colcombo<10, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-                case 11: colcombo<11, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-                case 12: colcombo<12, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-                case 13: colcombo<13, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-                case 14: colcombo<14, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-                default: colcombo<15, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-              }
-            }
-            break;
+          default: colcombo<7, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
         }
       }
-      if (TW % 3 != 0 && !kAsmCombo && __builtin_expect(cA + 2 >= TW, 0)) {   // straddles tile columns tA, tA + 1
+      if (TW == 8 && !kAsmCombo && __builtin_expect(cA + 2 >= TW, 0)) {   // straddles tile columns tA, tA + 1
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          zq[r] += TCN == 32 ? dpp_wshl1(zq[r]) : dpp_shl1(zq[r]);
-          rq[r] += TCN == 32 ? dpp_wshl1(rq[r]) : dpp_shl1(rq[r]);
+          zq[r] += dpp_shl1(zq[r]);
+          rq[r] += dpp_shl1(rq[r]);
         }
       }
       if (tc == tA) {

@@ -37,7 +37,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 REF = "/root/reference"
-HORIZONS = (10, 16, 20)
+HORIZONS = (10, 16, 20, 24, 32)
 
 
 def stub_reference(horizon):
@@ -76,13 +76,19 @@ def gen(horizon):
     names = ("a1", "aliengo")
     B = 16
     bt = make_batch(B, N, seed=4242 + N, gaits=gaits, robots=names)
+    if N > 20:
+        # the horizons only the interior-point class takes (N > kDenseN): beside the gait mix
+        # (standing robots included) a sparse schedule (n well below 128) and a flight one (n = 0)
+        rng = np.random.default_rng(777 + N)
+        bt["contact"][1] = (rng.random((N, 4)) < 0.2).astype(np.float32)
+        bt["contact"][2] = 0.0
     # per-robot records straight from the reference config classes
     robot_name = []
     for b in range(B):
         nm = "a1" if abs(bt["robot"][b][0] - 4.713) < 1e-3 else "aliengo"
         robot_name.append(nm)
         bt["robot"][b] = robot_from_config(cfgs[nm])
-    Hs, gs, us, kkts, iters = [], [], [], [], []
+    Hs, gs, us, kkts, iters, rounding = [], [], [], [], [], []
     C0 = lb0 = ub0 = None
     Cs, lbs, ubs = [], [], []
     for b in range(B):
@@ -103,18 +109,22 @@ def gen(horizon):
         us.append(x)
         kkts.append([k["stationarity"], k["primal"], k["dual"], k["complementarity"]])
         iters.append(info["iterations"])
-        if b < 2:
+        if b < (2 if N <= 20 else 1):
             Cs.append(C); lbs.append(lb); ubs.append(ub)
+        # u* is certified: the fixture is only as good as its optimum
+        assert max(kkts[-1]) < 1e-7, (N, b, kkts[-1])
+        rounding.append(len(info.get("rounding_accept", [])))
     # full H only for the first cases (size); every case keeps H @ probe vectors,
     # a size-independent pin of the whole matrix
-    nH = 2 if N <= 16 else 1
+    nH = 2 if N <= 16 else 1 if N <= 20 else 0
     probe = np.random.default_rng(99).standard_normal((2, 12 * N))
     probe[0] = 1.0
     Hprobe = np.array([[H @ v for v in probe] for H in Hs])
     out = dict(x0=bt["x0"], xref=bt["xref"], contact=bt["contact"], feet=bt["feet"], robot=bt["robot"],
                robot_name=np.array(robot_name), H=np.array(Hs[:nH]), H_probe=Hprobe, probe=probe,
                g=np.array(gs), u_star=np.array(us),
-               kkt=np.array(kkts), iterations=np.array(iters), C=np.array(Cs), lb=np.array(lbs),
+               kkt=np.array(kkts), iterations=np.array(iters), rounding_stops=np.array(rounding),
+               C=np.array(Cs), lb=np.array(lbs),
                ub=np.array(ubs), horizon=N, dt=0.05)
     np.savez_compressed(os.path.join(HERE, f"formulation_N{N}.npz"), **out)
 
@@ -130,7 +140,7 @@ def gen(horizon):
 
     if N == 16:
         gen_reftraj(LinearMpcConfig, robot_configs, mpc)
-    print(f"N={N}: max KKT {np.array(kkts).max():.2e}, iterations {iters}")
+    print(f"N={N}: max KKT {np.array(kkts).max():.2e}, iterations {iters}, rounding-level stops {rounding}")
 
 
 def full_weights(seed):

@@ -57,10 +57,12 @@ def test_u0_matches_oracle(N, gaits, robots, tilt):
     assert worst < TOL_ACHIEVED, worst
 
 
-@pytest.mark.parametrize("N", [10, 16, 20])
+@pytest.mark.parametrize("N", [10, 16, 20, 24, 32])
 def test_reference_golden_fixtures(N):
     """u* of QPs built by the reference's own functions (tests/golden/make_golden.py):
-    every case, standing schedules (n = 192 / 240, the interior-point class) included."""
+    every case, standing schedules (n = 192 / 240, the interior-point class) included; at
+    N = 24 / 32 (every robot in the interior-point class) also a sparse and a flight schedule,
+    held to that class's precision guard."""
     z = np.load(os.path.join(GOLDEN, f"formulation_N{N}.npz"), allow_pickle=False)
     bt = {k: z[k] for k in ("x0", "xref", "contact", "feet", "robot")}
     u0, U, status, _ = _solve(_engine(N), bt)
@@ -70,7 +72,9 @@ def test_reference_golden_fixtures(N):
         assert rel_err_u0(u0[b], z["u_star"][b][:12]) < TOL_U0, (b, u0[b], z["u_star"][b][:12])
         assert rel_err_u0(U[b], z["u_star"][b]) < TOL_U0, b
         worst = max(worst, rel_err_u0(u0[b], z["u_star"][b][:12]), rel_err_u0(U[b], z["u_star"][b]))
-    assert worst < TOL_ACHIEVED, worst
+    assert worst < (TOL_ACHIEVED if N <= 20 else TOL_ACHIEVED_IPM), worst
+    if N > 20:
+        assert np.all(U[2] == 0) and np.all(u0[2] == 0)   # the flight schedule
 
 
 @pytest.mark.parametrize("N", [10, 16])

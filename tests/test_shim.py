@@ -175,10 +175,12 @@ def test_shim_takes_full_weights():
 
 
 def test_shim_rejects_cross_leg_r_beyond_dense_classes():
-    """A cross-leg R entry is accepted at horizon 10 (12 N = 120: every schedule is dense),
-    and rejected at load time at horizon 16, where a standing schedule (n = 192) reaches
-    the interior-point class that takes leg-block R only.  Status 5 from the engine
-    (MPCQP_STATUS_UNSUPPORTED, U = 0) raises instead of returning zero forces."""
+    """A cross-leg R entry is accepted at horizon 10 (12 N = 120: every schedule is dense).
+    At horizon 16 it is accepted with a warning: trot / pace / bound schedules stay in the
+    dense classes (any symmetric R) and only a standing schedule (n = 192) reaches the
+    interior-point class, which takes leg-block R only -- such a tick raises on status 5
+    (MPCQP_STATUS_UNSUPPORTED, U = 0) instead of returning zero forces.  Beyond horizon 20
+    every schedule runs in that class, so the controller is rejected at load time."""
     m = _shim()
 
     class CrossR(LinearMpcConfig):
@@ -188,6 +190,9 @@ def test_shim_rejects_cross_leg_r_beyond_dense_classes():
     class CrossR16(CrossR):
         horizon = 16
 
+    class CrossR24(CrossR):
+        horizon = 24
+
     class LegBlockR16(LinearMpcConfig):
         horizon = 16
         R = LinearMpcConfig.R.copy()
@@ -195,8 +200,10 @@ def test_shim_rejects_cross_leg_r_beyond_dense_classes():
 
     m.ModelPredictiveController(CrossR, AliengoConfig)
     m.ModelPredictiveController(LegBlockR16, AliengoConfig)
-    with pytest.raises(ValueError, match="leg-block R"):
+    with pytest.warns(UserWarning, match="couples different legs"):
         m.ModelPredictiveController(CrossR16, AliengoConfig)
+    with pytest.raises(ValueError, match="leg-block R"):
+        m.ModelPredictiveController(CrossR24, AliengoConfig)
 
     c = m.ModelPredictiveController(LinearMpcConfig, AliengoConfig)
     class _Out:   # the pinned readback buffer's .numpy()
