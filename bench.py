@@ -63,6 +63,8 @@ def parse():
                     help="diagnostics: one HIP event pair per step (perturbs back-to-back dispatch, "
                          "~5%% slower steps); default: one pair around the timed loop")
     ap.add_argument("--no-callers", action="store_true", help="skip the planner/torque kernel timing")
+    ap.add_argument("--order", type=int, default=1, choices=(0, 1),
+                    help="dispatch order (mpcqp_set_order): 1 = largest predicted solve time first, 0 = batch order")
     ap.add_argument("--no-hint-line", action="store_true",
                     help="skip the no_hint sub-line (the default caller path without a stance promise)")
     ap.add_argument("--event-every", type=int, default=8,
@@ -455,6 +457,7 @@ def main():
     # and the smallest: the first capacity class any robot needs takes the batch directly
     # (mpcqp_set_stance_range; an all-standing fleet goes straight to the interior-point class)
     eng.set_stance_range(min_stance, max_stance)
+    eng.set_order(args.order)
     if args.warm_fleet:
         eng.set_warm_start(Bpg)
     dev_b = []
@@ -667,6 +670,7 @@ def main():
             "iters_max": int(it_all.max()),
             "status_ok_frac": float((st == 0).mean()),
             "stance_range": [min_stance, max_stance],
+            "dispatch_order": "predicted cost, largest first" if args.order else "batch order",
             "callers": callers,
         }
         if traffic_note:

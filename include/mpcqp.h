@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define MPCQP_ABI_VERSION 5
+#define MPCQP_ABI_VERSION 6
 #define MPCQP_ROBOT_STRIDE 16
 #define MPCQP_MAX_HORIZON 32   /* mpcqp_create rejects horizon > 32 (MPCQP_ERR_ARG).  Horizons
                                   up to 20 use every capacity class; longer ones are solved by
@@ -136,6 +136,16 @@ int mpcqp_set_stance_hint(mpcqp_ctx* ctx, int32_t max_stance);
  * MPCQP_ERR_ARG when min_stance > 4 * horizon (no schedule has that many) or
  * min_stance > max_stance > 0. */
 int mpcqp_set_stance_range(mpcqp_ctx* ctx, int32_t min_stance, int32_t max_stance);
+
+/* Dispatch order (ABI 6; the reference solves one robot at a time and has no batch order).
+ * mode 1 (the default): each launch's robots are dealt to workgroups largest predicted solve
+ * time first -- the key is the robot's horizontal velocity error |v0 - vref_0|, which tracks
+ * its active-set size -- so that a batch queueing on the CUs starts its longest robots first
+ * and a batch that fits the chip at once puts its heaviest robots on different CUs.  Costs one
+ * small sort launch per solve (batches >= 64 robots whose first class is a dense one); the
+ * results are bitwise those of mode 0 (batch order: robot b on workgroup b).
+ * MPCQP_ERR_ARG for any other mode. */
+int mpcqp_set_order(mpcqp_ctx* ctx, int32_t mode);
 
 /* Warm start (ABI 5; no counterpart in the reference, whose Drake solve starts cold every
  * MPC tick, mpc.py:277-286): per-robot memory of the last verified active set, for

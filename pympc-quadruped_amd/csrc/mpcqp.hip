@@ -67,6 +67,9 @@ static_assert(MPCQP_WARM_BYTES == 4 * kMaxN, "warm-start memory: one byte per (s
 #ifndef MPCQP_PRIO_V
 #define MPCQP_PRIO_V 0   // A/B only: class 64's issue priority from its start's violated-row count (>= V, V + 4, V + 8)
 #endif
+#ifndef MPCQP_PRIO_F
+#define MPCQP_PRIO_F 0   // A/B only: class 64's issue priority from the robot's velocity error (1: three bins, 2: one)
+#endif
 #ifndef MPCQP_ASM_COMBO
 // class 64's z / r column combination as one computed jump (mpcqp_combo_asm.h) instead of
 // the compiler's branch tree over an 8-way switch
@@ -355,6 +358,70 @@ __device__ __forceinline__ int xcd_robot(int bid, int B) {
   return x * q + (x < r ? x : r) + i;
 }
 
+// ---- Dispatch order (ABI 6, mpcqp_set_order).  A robot's active set -- and so its solve
+// time -- grows with the horizontal velocity correction its cone forces must supply: on the
+// benchmark batches |v0 - vref_0| has correlation 0.87 (config 2) / 0.85 (config 4) with the
+// iteration count (tools/order_sim.py).  mpcqp_order_kernel sorts each dispatch segment by
+// that key, largest first, so that (a) in a batch that queues on the CUs (configs 3 to 5) the
+// longest robots start first and the launch ends near its mean load instead of behind a late
+// long robot, and (b) in a batch that fits the chip at once (config 2) the heaviest robots are
+// the first ones dealt to each CU -- one per CU -- instead of meeting on a CU by chance.  Only
+// the robot -> workgroup map changes: every robot's solve is bitwise the same.
+constexpr int kOrderMax = 8192;   // robots per sorted segment (one workgroup, 64 KB of LDS)
+constexpr int kOrderMin = 64;     // smaller batches keep their order (nothing to balance)
+
+__device__ __forceinline__ float order_key(const float* __restrict__ x0g, const float* __restrict__ xrefg, int N,
+                                           int r) {
+  const float ex = x0g[(size_t)r * NX + 9] - xrefg[(size_t)r * N * NX + 9];
+  const float ey = x0g[(size_t)r * NX + 10] - xrefg[(size_t)r * N * NX + 10];
+  const float k = ex * ex + ey * ey;
+  return k >= 0.0f && k <= 3.0e38f ? k : 0.0f;   // NaN / inf: no preference
+}
+
+// One workgroup per segment.  mode 0: segment x = class 64's XCD range x (xcd_robot: the robots
+// of blocks x, x + 8, ...), so a sorted range keeps its robots on their XCD's L2; mode 1:
+// consecutive segments of kOrderMax robots (the direct launches of classes 96 / 128, one robot
+// per CU at a time).  perm[lo + j] = the robot of the segment with the j-th largest key (ties:
+// lower index first).
+__global__ __launch_bounds__(1024) void mpcqp_order_kernel(int B, int N, const float* __restrict__ x0g,
+                                                           const float* __restrict__ xrefg, int* __restrict__ perm,
+                                                           int mode) {
+  __shared__ unsigned long long key[kOrderMax];
+  const int seg = blockIdx.x, tid = threadIdx.x;
+  int lo, len;
+  if (mode == 0) {
+    const int q = B >> 3, r = B & 7;
+    lo = seg * q + (seg < r ? seg : r);
+    len = q + (seg < r ? 1 : 0);
+  } else {
+    lo = seg * kOrderMax;
+    len = B - lo < kOrderMax ? B - lo : kOrderMax;
+  }
+  if (len <= 0) return;
+  int P = 1;
+  while (P < len) P <<= 1;
+  // (key bits, ~index): non-negative float keys order as their bit patterns; pads are 0 (last)
+  for (int j = tid; j < P; j += 1024)
+    key[j] = j < len ? ((unsigned long long)__float_as_uint(order_key(x0g, xrefg, N, lo + j)) << 32) |
+                           (unsigned long long)(0xffffffffu - (unsigned)j)
+                     : 0ull;
+  __syncthreads();
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = tid; t < (P >> 1); t += 1024) {
+        const int i = 2 * j * (t / j) + (t % j), l = i + j;
+        const unsigned long long a = key[i], c = key[l];
+        if ((a < c) == ((i & k) == 0)) {   // bitonic merge, descending overall
+          key[i] = c;
+          key[l] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int j = tid; j < len; j += 1024) perm[lo + j] = lo + (int)(0xffffffffu - (unsigned)(key[j] & 0xffffffffull));
+}
+
 // class 64's capacity (stance variables)
 constexpr int kCap64 = 64;
 // interior-point class: global S_k slots per CU.  Every layout takes more than a fifth of a
@@ -379,9 +446,10 @@ __global__ __launch_bounds__(Cfg<64>::NT) __attribute__((amdgpu_waves_per_eu(2, 
     KParams P, int B, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
-    int* __restrict__ queue, int* __restrict__ queue_big, int* __restrict__ queue_ipm) {
+    int* __restrict__ queue, int* __restrict__ queue_big, int* __restrict__ queue_ipm, const int* __restrict__ perm) {
   if ((int)blockIdx.x >= B) return;
-  const int b = xcd_robot(blockIdx.x, B);
+  int b = xcd_robot(blockIdx.x, B);
+  if (perm) b = uni(perm[b]);   // the dispatch order (mpcqp_order_kernel, mode 0)
   __shared__ SharedT<64> sm;
   solve_robot<64, FULL>(P, b, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, queue, queue_big,
                   queue_ipm);
@@ -396,13 +464,15 @@ __global__ __launch_bounds__(Cfg<96>::NT) __attribute__((amdgpu_waves_per_eu((Cf
     KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
-    int* __restrict__ queue, int* __restrict__ qout, int* __restrict__ q_ipm, int direct_B) {
+    int* __restrict__ queue, int* __restrict__ qout, int* __restrict__ q_ipm, int direct_B,
+    const int* __restrict__ perm) {
   __shared__ SharedT<96> sm;
   const int tid = threadIdx.x;
   const int k = blockIdx.x;
-  if (direct_B > 0) {   // the caller's stance range rules class 64 out: robot = workgroup
-    if (k < direct_B) solve_robot<96, FULL>(P, k, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg, qout,
-                                      nullptr, q_ipm);
+  if (direct_B > 0) {   // the caller's stance range rules class 64 out: robot = workgroup (or perm[k])
+    if (k < direct_B)
+      solve_robot<96, FULL>(P, perm ? uni(perm[k]) : k, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg,
+                            itersg, qout, nullptr, q_ipm);
     return;
   }
   const int cnt = uni(__hip_atomic_load(&queue[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -428,13 +498,14 @@ __global__ __launch_bounds__(Cfg<128>::NT) void mpcqp_kernel_128(
     KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
-    int* __restrict__ queue, int* __restrict__ q_ipm, int direct_B) {
+    int* __restrict__ queue, int* __restrict__ q_ipm, int direct_B, const int* __restrict__ perm) {
   __shared__ SharedT<128> sm;
   const int tid = threadIdx.x;
   const int k = blockIdx.x;
   if (direct_B > 0) {
-    if (k < direct_B) solve_robot<128, FULL>(P, k, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg, itersg,
-                                       q_ipm, nullptr, q_ipm);
+    if (k < direct_B)
+      solve_robot<128, FULL>(P, perm ? uni(perm[k]) : k, sm, x0g, xrefg, contactg, feetg, robotg, u0g, Ug, statusg,
+                             itersg, q_ipm, nullptr, q_ipm);
     return;
   }
   const int cnt = uni(__hip_atomic_load(&queue[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -473,8 +544,10 @@ __device__ __forceinline__ int ipm_claim_slot(unsigned* bits, int nw, int start)
 
 // Large class (n > 128, and every robot at N > 20): one wave per robot; its Riccati S_k in
 // a global slot claimed for the robot's solve (sbits: slot bitmap, nsw words)
+// One wave per SIMD at most (LDS bounds a CU to 3 or 4 of these workgroups): the wave may take
+// the whole 512-register file, so values beyond the 256 arch VGPRs live in AGPRs, not scratch
 template <bool FULL, int NM, bool MG = false>
-__global__ __launch_bounds__(LANES) void mpcqp_kernel_ipm(
+__global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(1, 1))) void mpcqp_kernel_ipm(
     KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
     float* __restrict__ u0g, float* __restrict__ Ug, int* __restrict__ statusg, int* __restrict__ itersg,
@@ -540,6 +613,7 @@ struct mpcqp_ctx {
   int device;
   int stance_hint;   // max stance foot-steps per robot promised by the caller (0: none)
   int stance_min;    // min stance foot-steps per robot promised by the caller
+  int order;         // dispatch order (mpcqp_set_order): 1 = predicted-cost order, 0 = batch order
   int ncu;
   std::vector<QueueSet> queues;
   unsigned long long use_clock;
@@ -634,7 +708,8 @@ static QueueSet* stream_queues(mpcqp_ctx* ctx, hipStream_t st, int batch, int* e
     qs->buf = nullptr;
     qs->cap = 0;
   }
-  const size_t bytes = sizeof(int) * 3 * (4 + (size_t)batch);
+  // three queues of 4 + batch ints, then the dispatch order (mpcqp_order_kernel) of batch ints
+  const size_t bytes = sizeof(int) * (3 * (4 + (size_t)batch) + (size_t)batch);
   if (hipMalloc(&qs->buf, bytes) != hipSuccess) {
     qs->buf = nullptr;
     *err = set_err(ctx, MPCQP_ERR_ALLOC, "queue allocation failed");
@@ -694,6 +769,7 @@ int mpcqp_create(const mpcqp_params* p, int32_t device, mpcqp_ctx** out) {
   ctx->device = device;
   ctx->stance_hint = 0;
   ctx->stance_min = 0;
+  ctx->order = 1;
   ctx->ncu = 0;
   ctx->use_clock = 0;
   ctx->sscratch = nullptr;
@@ -719,6 +795,13 @@ int mpcqp_set_warm_start(mpcqp_ctx* ctx, void* memory, int32_t capacity) {
     return set_err(ctx, MPCQP_ERR_ARG, "warm start: capacity < 0, or no memory for capacity > 0");
   ctx->warm = capacity > 0 ? static_cast<unsigned char*>(memory) : nullptr;
   ctx->warm_cap = capacity > 0 ? capacity : 0;
+  return MPCQP_OK;
+}
+
+int mpcqp_set_order(mpcqp_ctx* ctx, int32_t mode) {
+  if (!ctx) return MPCQP_ERR_ARG;
+  if (mode != 0 && mode != 1) return set_err(ctx, MPCQP_ERR_ARG, "order: mode must be 0 or 1");
+  ctx->order = mode;
   return MPCQP_OK;
 }
 
@@ -779,10 +862,14 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   // its side stream at once -- a dense class taking the batch directly would route its
   // standing robots only as its own workgroups run, and the fork would wait for all of it.
   const int first = ipm_only || nmin > 128 ? 3 : giant ? 0 : nmin > 96 ? 2 : nmin > kCap64 ? 1 : 0;
+  // the dispatch order (mpcqp_order_kernel) of the first class's launch: class 64 sorts its 8 XCD
+  // ranges (each <= kOrderMax robots), classes 96 / 128 taking the batch directly sort segments
+  // of kOrderMax; the interior-point class and small batches keep the batch order
+  const bool use_order = ctx->order && batch >= kOrderMin && first < 3 && (first > 0 || batch <= 8 * kOrderMax);
   int* q = nullptr;
   QueueSet* qs = nullptr;
   int cap = 0;
-  if (large) {
+  if (large || use_order) {
     int qerr = MPCQP_OK;
     qs = stream_queues(ctx, st, batch, &qerr, &cap);
     if (!qs) return qerr;
@@ -839,8 +926,9 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
     if (hipEventRecord(qs->ev_join, qs->side) != hipSuccess) return set_err(ctx, MPCQP_ERR_HIP, "join record failed");
     return MPCQP_OK;
   };
-  const size_t qstride = 4 + (size_t)cap;   // the set's layout: three queues of 4 + cap ints
+  const size_t qstride = 4 + (size_t)cap;   // the set's layout: three queues of 4 + cap ints, the order
   int* q1 = large ? q : nullptr;
+  int* perm = use_order ? q + 3 * qstride : nullptr;
   int* q2 = huge ? q + qstride : nullptr;
   int* q3 = giant ? q + 2 * qstride : nullptr;
   hipError_t e = hipSuccess;
@@ -851,23 +939,32 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
     if (qs) (void)hipEventRecord(qs->ev_done, st);
     return code;
   };
+  if (use_order) {
+    const int segs = first == 0 ? 8 : (int)((batch + kOrderMax - 1) / kOrderMax);
+    hipLaunchKernelGGL(mpcqp_order_kernel, dim3(segs), dim3(1024), 0, st, (int)batch, kp.N, x0, xref, perm,
+                       first == 0 ? 0 : 1);
+    e = hipGetLastError();
+    if (e != hipSuccess) return failed(set_err(ctx, MPCQP_ERR_HIP, std::string("launch (order): ") + hipGetErrorString(e)));
+  }
   if (first == 0) {
     hipLaunchKernelGGL(full ? mpcqp_kernel_64<true> : mpcqp_kernel_64<false>, dim3(batch), dim3(Cfg<64>::NT), 0, st, kp, (int)batch, x0, xref, contact,
-                       feet, robot, u0, U, (int*)status, (int*)iters, q1, q2, q3);
+                       feet, robot, u0, U, (int*)status, (int*)iters, q1, q2, q3, perm);
     e = hipGetLastError();
     if (e != hipSuccess) return failed(set_err(ctx, MPCQP_ERR_HIP, std::string("launch: ") + hipGetErrorString(e)));
     if ((fe = fork_ipm()) != MPCQP_OK) return failed(fe);
   }
   if (large && first <= 1) {
     hipLaunchKernelGGL(full ? mpcqp_kernel_96<true> : mpcqp_kernel_96<false>, dim3(batch), dim3(Cfg<96>::NT), 0, st, kp, x0, xref, contact, feet, robot,
-                       u0, U, (int*)status, (int*)iters, q1, q2, q3, first == 1 ? (int)batch : 0);
+                       u0, U, (int*)status, (int*)iters, q1, q2, q3, first == 1 ? (int)batch : 0,
+                       first == 1 ? perm : nullptr);
     e = hipGetLastError();
     if (e != hipSuccess) return failed(set_err(ctx, MPCQP_ERR_HIP, std::string("launch (96): ") + hipGetErrorString(e)));
     if ((fe = fork_ipm()) != MPCQP_OK) return failed(fe);
   }
   if (huge && first <= 2) {
     hipLaunchKernelGGL(full ? mpcqp_kernel_128<true> : mpcqp_kernel_128<false>, dim3(batch), dim3(Cfg<128>::NT), 0, st, kp, x0, xref, contact, feet, robot,
-                       u0, U, (int*)status, (int*)iters, q2, q3, first == 2 ? (int)batch : 0);
+                       u0, U, (int*)status, (int*)iters, q2, q3, first == 2 ? (int)batch : 0,
+                       first == 2 ? perm : nullptr);
     e = hipGetLastError();
     if (e != hipSuccess) return failed(set_err(ctx, MPCQP_ERR_HIP, std::string("launch (128): ") + hipGetErrorString(e)));
     if ((fe = fork_ipm()) != MPCQP_OK) return failed(fe);

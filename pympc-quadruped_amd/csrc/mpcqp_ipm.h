@@ -371,86 +371,6 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     return (a0 + a1) + (a2 + a3);
   };
 
-  // sm.gr = H U + g on stance coordinates: forward simulation + adjoint recursion
-  auto gradient = [&]() {
-    IPM_T0();
-    for (int e = lane; e < N * NU; e += NT) {   // B_d U_k, every stage
-      const int k = e / NU, i = e % NU;
-      double bi[12], u[12];
-      ld12(bi, sm.Bm[i]);
-      ld12(u, sm.U[k]);
-      sm.BU[k][i] = dot12(bi, u);
-    }
-    fsync<NT>();
-    // x_{k+1} = x_k + Nm x_k + B_d u_k (lane 12, the gravity state, stays constant)
-    double x = lane < NX ? sm.x0[lane] : 0.0;
-    if (lane < NX) sm.X[0][lane] = x;
-    for (int k = 0; k < N; ++k) {
-      const double bu = sm.BU[k][lane < NU ? lane : 0];
-      double s[7];
-#pragma unroll
-      for (int t = 0; t < 7; ++t) s[t] = readlane_d(x, 6 + t);
-      x += mix7(fc, s, lane < NU ? bu : 0.0);
-      if (lane < NX) sm.X[k + 1][lane] = x;   // read back by the same lane below
-    }
-    // nu_k = Qh (x_{k+1} - xref_k) + (I + Nm^T) nu_{k+1}
-    double nu = 0.0;
-    const int li = lane < NX ? lane : 0;
-    for (int k = N - 1; k >= 0; --k) {
-      double v = 0.0;
-      if constexpr (FULL) {
-        if (lane < NX) {
-#pragma unroll
-          for (int j = 0; j < NX; ++j) v = fma(sm.wf.qf[li][j], sm.X[k + 1][j] - sm.xr[k][j], v);
-        }
-      } else {
-        v = lane < NX ? sm.qh[li] * (sm.X[k + 1][li] - sm.xr[k][li]) : 0.0;
-      }
-      if (k < N - 1) {
-        double s[7];
-#pragma unroll
-        for (int t = 0; t < 6; ++t) s[t] = readlane_d(nu, t);
-        s[6] = readlane_d(nu, 11);
-        v += nu + mix7(bc, s, 0.0);
-      }
-      nu = v;
-      if (lane < NU) sm.nuh[k][lane] = nu;
-    }
-    fsync<NT>();
-    for (int e = lane; e < N * NU; e += NT) {   // stage gradients R u_k + B_d^T nu_k
-      const int k = e / NU, c = e % NU;
-      double bcl[12], nv[12];
-      ld12(bcl, sm.BmT[c]);
-      ld12(nv, sm.nuh[k]);
-      double ru;
-      if constexpr (FULL) {
-        const int c3 = 3 * (c / 3);   // Rh's leg block (no cross-leg couplings in this class)
-        ru = fma(sm.wf.rf[c][c3 + 2], sm.U[k][c3 + 2], fma(sm.wf.rf[c][c3 + 1], sm.U[k][c3 + 1], sm.wf.rf[c][c3] * sm.U[k][c3]));
-      } else {
-        ru = sm.rh[c] * sm.U[k][c];
-      }
-      const double g = ru + dot12(bcl, nv);
-      sm.gr[k][c] = sm.mt.stance_of[4 * k + c / 3] >= 0 ? g : 0.0;
-    }
-    fsync<NT>();
-    IPM_T1(0);
-  };
-
-  // Riccati factorisation with the per-foot-step weights sm.W: S_k and M_k for every
-  // stage, the 12 x 12 stage products on the f64 matrix cores.  v_mfma_f64_16x16x4f64
-  // (tools/ubench/mfma_f64_check.hip; lr = lane >> 4, lc = lane & 15): the A operand of
-  // K-chunk q is A[lc][4q + lr], the B operand B[4q + lr][lc], result register i
-  // D[lr + 4i][lc] -- so result register q of a matrix IS its B operand of chunk q, and
-  // its A operand when the matrix is symmetric; the recursion P -> T -> S -> P stays in
-  // registers (12 x 12 padded to 16 x 16) except for the Gauss-Jordan sweep.  Per stage:
-  //   E = B_d blockdiag(W_k) B_d^T   (blockdiag(W_k) B_d^T formed on the VALU in B-operand form)
-  //   T = I + P E;  S = T^-1 P by Gauss-Jordan on [T | P] (lane j < 12 holds column j of T,
-  //       lane 12 + j column j of P; pivot column by readlane), symmetrised
-  //   P <- Qh + A^T S A;  M_k = A^T (I - S E)     (A = I + Nm; Nm has rows 0..5 only, so
-  //       a product with Nm or Nm^T is 2 K-chunks)
-  // (information form; the textbook P - P B (R + B^T P B)^-1 B^T P loses ~4 digits here).
-  // The critical path per stage is S -> P -> T -> sweep; E of the next stage and M of the
-  // previous one are issued before the sweep, so the matrix cores run them under it.
   const int lr = lane >> 4, lc = lane & 15;
   const int lcc = lc < 12 ? lc : 0;
   double Nmb[2], Bop[3], bx[3][3];   // Nm[4q+lr][lc]; B_d[lc][4q+lr]; B_d[lc][3 leg(4q+lr) + a]
@@ -486,6 +406,111 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     return v;
   };
   auto mfma = [](double a, double b, d4 c) -> d4 { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); };
+  // dst_k = src_k M^T for every stage k < N, M = B_d (bop = Bop) or B_d^T (bop = BmT's operands):
+  // the N x 12 by 12 x 12 product on the f64 matrix cores, 16 stages per tile -- per K-chunk one
+  // 8-byte LDS read and one v_mfma_f64_16x16x4_f64 per lane, in place of two whole 12-vector reads
+  // per output entry (the batched phases' LDS traffic bounds the class at four robots per CU)
+  auto stage_gemm = [&](double (*dst)[NU], const double (*src)[NU], const double (&bop)[3]) {
+    for (int t = 0; t < N; t += 16) {
+      d4 D = diag4(0.0);
+      const int ka = t + lc;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int j = 4 * q + lr;
+        D = mfma(ka < N && j < 12 ? src[ka][j] : 0.0, bop[q], D);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = t + lr + 4 * i;
+        if (k < N && lc < 12) dst[k][lc] = D[i];
+      }
+    }
+    fsync<NT>();
+  };
+  // B_d^T's B operands: B_d[4q + lr][lc] (BmT is B_d^T, row lc)
+  auto bt_ops = [&](double (&bt)[3]) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int c = 4 * q + lr;
+      bt[q] = c < 12 && lc < 12 ? sm.BmT[lc][c] : 0.0;
+    }
+  };
+
+  // sm.gr = H U + g on stance coordinates: forward simulation + adjoint recursion
+  auto gradient = [&]() {
+    IPM_T0();
+    stage_gemm(sm.BU, sm.U, Bop);   // B_d U_k, every stage
+    // x_{k+1} = x_k + Nm x_k + B_d u_k (lane 12, the gravity state, stays constant)
+    double x = lane < NX ? sm.x0[lane] : 0.0;
+    if (lane < NX) sm.X[0][lane] = x;
+    for (int k = 0; k < N; ++k) {
+      const double bu = sm.BU[k][lane < NU ? lane : 0];
+      double s[7];
+#pragma unroll
+      for (int t = 0; t < 7; ++t) s[t] = readlane_d(x, 6 + t);
+      x += mix7(fc, s, lane < NU ? bu : 0.0);
+      if (lane < NX) sm.X[k + 1][lane] = x;   // read back by the same lane below
+    }
+    // nu_k = Qh (x_{k+1} - xref_k) + (I + Nm^T) nu_{k+1}
+    double nu = 0.0;
+    const int li = lane < NX ? lane : 0;
+    for (int k = N - 1; k >= 0; --k) {
+      double v = 0.0;
+      if constexpr (FULL) {
+        if (lane < NX) {
+#pragma unroll
+          for (int j = 0; j < NX; ++j) v = fma(sm.wf.qf[li][j], sm.X[k + 1][j] - sm.xr[k][j], v);
+        }
+      } else {
+        v = lane < NX ? sm.qh[li] * (sm.X[k + 1][li] - sm.xr[k][li]) : 0.0;
+      }
+      if (k < N - 1) {
+        double s[7];
+#pragma unroll
+        for (int t = 0; t < 6; ++t) s[t] = readlane_d(nu, t);
+        s[6] = readlane_d(nu, 11);
+        v += nu + mix7(bc, s, 0.0);
+      }
+      nu = v;
+      if (lane < NU) sm.nuh[k][lane] = nu;
+    }
+    fsync<NT>();
+    {
+      double bt[3];
+      bt_ops(bt);
+      stage_gemm(sm.BU, sm.nuh, bt);   // B_d^T nu_k, every stage (B_d U_k is dead)
+    }
+    for (int e = lane; e < N * NU; e += NT) {   // stage gradients R u_k + B_d^T nu_k
+      const int k = e / NU, c = e % NU;
+      double ru;
+      if constexpr (FULL) {
+        const int c3 = 3 * (c / 3);   // Rh's leg block (no cross-leg couplings in this class)
+        ru = fma(sm.wf.rf[c][c3 + 2], sm.U[k][c3 + 2], fma(sm.wf.rf[c][c3 + 1], sm.U[k][c3 + 1], sm.wf.rf[c][c3] * sm.U[k][c3]));
+      } else {
+        ru = sm.rh[c] * sm.U[k][c];
+      }
+      const double g = ru + sm.BU[k][c];
+      sm.gr[k][c] = sm.mt.stance_of[4 * k + c / 3] >= 0 ? g : 0.0;
+    }
+    fsync<NT>();
+    IPM_T1(0);
+  };
+
+  // Riccati factorisation with the per-foot-step weights sm.W: S_k and M_k for every
+  // stage, the 12 x 12 stage products on the f64 matrix cores.  v_mfma_f64_16x16x4f64
+  // (tools/ubench/mfma_f64_check.hip; lr = lane >> 4, lc = lane & 15): the A operand of
+  // K-chunk q is A[lc][4q + lr], the B operand B[4q + lr][lc], result register i
+  // D[lr + 4i][lc] -- so result register q of a matrix IS its B operand of chunk q, and
+  // its A operand when the matrix is symmetric; the recursion P -> T -> S -> P stays in
+  // registers (12 x 12 padded to 16 x 16) except for the Gauss-Jordan sweep.  Per stage:
+  //   E = B_d blockdiag(W_k) B_d^T   (blockdiag(W_k) B_d^T formed on the VALU in B-operand form)
+  //   T = I + P E;  S = T^-1 P by Gauss-Jordan on [T | P] (lane j < 12 holds column j of T,
+  //       lane 12 + j column j of P; pivot column by readlane), symmetrised
+  //   P <- Qh + A^T S A;  M_k = A^T (I - S E)     (A = I + Nm; Nm has rows 0..5 only, so
+  //       a product with Nm or Nm^T is 2 K-chunks)
+  // (information form; the textbook P - P B (R + B^T P B)^-1 B^T P loses ~4 digits here).
+  // The critical path per stage is S -> P -> T -> sweep; E of the next stage and M of the
+  // previous one are issued before the sweep, so the matrix cores run them under it.
   auto stage_e = [&](int k) -> d4 {   // E_k
     d4 Er = diag4(0.0);
 #pragma unroll
@@ -609,32 +634,21 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
   //                                              = M_k^T dx_k + B (W_k B^T S_k B Y_k - Y_k),
   // so each recursion is one 12 x 12 matvec per stage (12 lanes, readlane of the vector)
   // and every other product runs for all stages at once.
-  // W_k B^T x restricted to entry c (leg l = c / 3): the leg's 3 x 3 weight row times the
-  // leg's three B_d columns against x; 0 for a swing leg
-  auto wbt = [&](int k, int c, const double (&x)[12], const double (*sub)) -> double {
+  auto bmat = [&](double (*dst)[NU], double (*src)[NU]) { stage_gemm(dst, src, Bop); };   // dst_k = B_d src_k
+  // W_k (z_k - sub_k) restricted to entry c (leg l = c / 3), z_k = B_d^T x_k precomputed for every
+  // stage by stage_gemm; 0 for a swing leg
+  auto wz = [&](int k, int c, const double (*z)[NU], const double* sub) -> double {
     const int l = c / 3, a = c % 3;
     const int j = sm.mt.stance_of[4 * k + l];
     if (j < 0) return 0.0;
-    double b0[12], b1[12], b2[12];
-    ld12(b0, sm.BmT[3 * l]);
-    ld12(b1, sm.BmT[3 * l + 1]);
-    ld12(b2, sm.BmT[3 * l + 2]);
-    const double z0 = dot12(b0, x) - (sub ? sub[3 * l] : 0.0);
-    const double z1 = dot12(b1, x) - (sub ? sub[3 * l + 1] : 0.0);
-    const double z2 = dot12(b2, x) - (sub ? sub[3 * l + 2] : 0.0);
+    const double z0 = z[k][3 * l] - (sub ? sub[3 * l] : 0.0);
+    const double z1 = z[k][3 * l + 1] - (sub ? sub[3 * l + 1] : 0.0);
+    const double z2 = z[k][3 * l + 2] - (sub ? sub[3 * l + 2] : 0.0);
     const double* wj = sm.W[j] + 3 * a;
     return wj[0] * z0 + wj[1] * z1 + wj[2] * z2;
   };
-  auto bmat = [&](double (*dst)[NU], double (*src)[NU]) {   // dst_k = B_d src_k, every stage
-    for (int e = lane; e < N * NU; e += NT) {
-      const int k = e / NU, i = e % NU;
-      double bi[12], v[12];
-      ld12(bi, sm.Bm[i]);
-      ld12(v, src[k]);
-      dst[k][i] = dot12(bi, v);
-    }
-    fsync<NT>();
-  };
+  double btop[3];   // B_d^T's operands for the lsolve phases
+  bt_ops(btop);
   auto smat = [&](double (*dst)[NU], double (*src)[NU]) {   // dst_k = S_k src_k, every stage
     for (int e = lane; e < N * NU; e += NT) {
       const int k = e / NU, i = e % NU;
@@ -702,20 +716,18 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       }
     }
     fsync<NT>();
+    stage_gemm(sm.la, sm.ph, btop);   // B^T p_{k+1} (la is dead until S B Y below)
     for (int e = lane; e < N * NU; e += NT) {   // Y_k = W_k (B^T p_{k+1} - rhs_k)
       const int k = e / NU, c = e % NU;
-      double pk[12];
-      ld12(pk, sm.ph[k]);
-      sm.Y[k][c] = wbt(k, c, pk, sm.rhs[k]);
+      sm.Y[k][c] = wz(k, c, sm.la, sm.rhs[k]);
     }
     fsync<NT>();
     bmat(sm.By, sm.Y);    // B Y
     smat(sm.la, sm.By);   // S B Y
+    stage_gemm(sm.lc, sm.la, btop);   // B^T S B Y (lc is dead until B lb below)
     for (int e = lane; e < N * NU; e += NT) {   // lb_k = W_k B^T S_k B Y_k - Y_k
       const int k = e / NU, c = e % NU;
-      double sk[12];
-      ld12(sk, sm.la[k]);
-      sm.lb[k][c] = wbt(k, c, sk, nullptr) - sm.Y[k][c];
+      sm.lb[k][c] = wz(k, c, sm.lc, nullptr) - sm.Y[k][c];
     }
     fsync<NT>();
     bmat(sm.lc, sm.lb);   // B lb
@@ -768,11 +780,10 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       sm.la[k][i] = dot12(sr, by);
     }
     fsync<NT>();
+    stage_gemm(sm.lb, sm.la, btop);   // B^T la_k (lb is dead after B lb)
     for (int e = lane; e < N * NU; e += NT) {   // d_k = W_k B^T la_k - Y_k
       const int k = e / NU, c = e % NU;
-      double w[12];
-      ld12(w, sm.la[k]);
-      sm.dU[k][c] = wbt(k, c, w, nullptr) - sm.Y[k][c];
+      sm.dU[k][c] = wz(k, c, sm.lb, nullptr) - sm.Y[k][c];
     }
     fsync<NT>();
     IPM_T1(2);

@@ -229,6 +229,24 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   }
   if (wave == 0) form_stance(smf, sm.mt, N, lane);
   fsync<NT>();
+#if MPCQP_PRIO_F > 0
+  // A/B: issue priority from the robot's horizontal velocity error |v0 - vref_0| (its QP's
+  // active set grows with the correction the cone must supply: corr 0.87 with the iteration
+  // count on config 2), so a likely-long robot is not slowed by the robots sharing its SIMDs
+  if constexpr (NV == 64) {
+    using FT = std::remove_reference_t<decltype(smf)>;
+    const float ex = smf.in[IN_X0 + 9] - smf.in[FT::IN_XREF + 9];
+    const float ey = smf.in[IN_X0 + 10] - smf.in[FT::IN_XREF + 10];
+    const float e2 = ex * ex + ey * ey;
+    if (MPCQP_PRIO_F == 1) {
+      if (e2 >= 1.8f * 1.8f) __builtin_amdgcn_s_setprio(3);
+      else if (e2 >= 1.4f * 1.4f) __builtin_amdgcn_s_setprio(2);
+      else if (e2 >= 1.0f * 1.0f) __builtin_amdgcn_s_setprio(1);
+    } else {
+      if (e2 >= 1.4f * 1.4f) __builtin_amdgcn_s_setprio(1);
+    }
+  }
+#endif
   const int S = uni(sm.mt.S);
   const int n = 3 * S, m = 6 * S;
   if (n > NV) {

@@ -32,6 +32,7 @@ EXPORTED_SYMBOLS = (
     "mpcqp_solve",
     "mpcqp_set_stance_hint",
     "mpcqp_set_stance_range",
+    "mpcqp_set_order",
     "mpcqp_set_weights",
     "mpcqp_set_warm_start",
     "mpcqp_destroy",
@@ -41,7 +42,7 @@ EXPORTED_SYMBOLS = (
     "mpcqp_set_planner",
     "mpcqp_stance_torques",
 )
-ABI_VERSION = 5
+ABI_VERSION = 6
 WARM_BYTES = 128     # MPCQP_WARM_BYTES: warm-start memory per robot
 PLAN_STRIDE = 8     # MPCQP_PLAN_STRIDE: float64 planner state per robot
 GAIT_STRIDE = 9     # MPCQP_GAIT_STRIDE: period, offsets[4], durations[4]
@@ -89,6 +90,8 @@ def load():
     lib.mpcqp_set_stance_hint.argtypes = [vp, i32]
     lib.mpcqp_set_stance_range.restype = ctypes.c_int
     lib.mpcqp_set_stance_range.argtypes = [vp, i32, i32]
+    lib.mpcqp_set_order.restype = ctypes.c_int
+    lib.mpcqp_set_order.argtypes = [vp, i32]
     lib.mpcqp_set_weights.restype = ctypes.c_int
     lib.mpcqp_set_weights.argtypes = [vp, vp, vp]
     lib.mpcqp_set_warm_start.restype = ctypes.c_int

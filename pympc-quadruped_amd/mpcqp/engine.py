@@ -121,6 +121,12 @@ class LinearMpc:
             _lib.check(self._ctx, self.lib.mpcqp_set_stance_range(self._ctx, *rng), "set_stance_range")
             self._hint = rng
 
+    def set_order(self, mode):
+        """Dispatch order of the following solves (include/mpcqp.h mpcqp_set_order): 1 (the
+        default) deals each launch's robots to workgroups largest predicted solve time first,
+        0 keeps the batch order.  Results are bitwise the same either way."""
+        _lib.check(self._ctx, self.lib.mpcqp_set_order(self._ctx, int(mode)), "mpcqp_set_order")
+
     def set_warm_start(self, capacity):
         """Remember each robot's verified active set between solves (include/mpcqp.h
         mpcqp_set_warm_start): robot b of every later solve starts the interior-point class

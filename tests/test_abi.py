@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     lib = _lib.load()
     for name in _declared():
         assert hasattr(lib, name), name
-    assert lib.mpcqp_abi_version() == _lib.ABI_VERSION == 5
+    assert lib.mpcqp_abi_version() == _lib.ABI_VERSION == 6
 
 
 def test_params_struct_layout():
@@ -54,6 +54,7 @@ def test_create_rejects_bad_arguments_without_crashing():
     assert lib.mpcqp_solve(None, 1, None, None, None, None, None, None, None, None, None, None) == -1
     assert lib.mpcqp_set_stance_hint(None, 3) == -1
     assert lib.mpcqp_set_stance_range(None, 1, 3) == -1
+    assert lib.mpcqp_set_order(None, 1) == -1
     assert lib.mpcqp_plan(None, 1, 1, *([None] * 15)) == -1
     assert lib.mpcqp_plan_root_states(None, 1, 1, *([None] * 11)) == -1
     assert lib.mpcqp_stance_torques(None, 1, None, None, 4, None, None, None) == -1

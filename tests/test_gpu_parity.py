@@ -57,6 +57,34 @@ def test_u0_matches_oracle(N, gaits, robots, tilt):
     assert worst < TOL_ACHIEVED, worst
 
 
+@pytest.mark.parametrize("N,B,gaits,robots,tilt,first", [
+    (10, 1024, ("trot10",), ("a1",), 0.0, 0),                                    # config 2: one launch of class 64
+    (10, 3000, ("trot10", "pace10", "bound8"), ("a1", "aliengo"), 0.0, 0),       # queued class 64, uneven XCD ranges
+    (16, 700, ("trot10", "pace10", "bound8"), ("a1",), 0.0, 1),                  # class 96 taking the batch directly
+    (20, 300, ("trot10", "pace10", "bound8"), ("a1", "aliengo"), 15.0, 2),       # class 128 directly
+])
+def test_dispatch_order_is_bitwise_neutral(N, B, gaits, robots, tilt, first):
+    """mpcqp_set_order (ABI 6): dealing robots to workgroups by predicted cost changes only
+    which workgroup solves a robot -- u0, U, status and iterations are bitwise those of the
+    batch order, for class 64 (its XCD ranges sorted) and for classes 96 / 128 taking the
+    batch directly (their segments sorted)."""
+    from mpcqp.synthetic import make_batch
+    bt = make_batch(B, N, seed=900 + N, gaits=gaits, robots=robots, tilt_deg=tilt)
+    stance = (bt["contact"] > 0).reshape(B, -1).sum(1)
+    out = []
+    for mode in (0, 1):
+        eng = _engine(N)
+        if first:
+            eng.set_stance_range(int(stance.min()), int(stance.max()))
+        eng.set_order(mode)
+        out.append(_solve(eng, bt))
+    for a, b in zip(out[0], out[1]):
+        assert np.array_equal(a, b)
+    assert (out[1][2] == 0).all()
+    x, _, _ = oracle_solution(bt, B - 1, N)
+    assert rel_err_u0(out[1][0][B - 1], x[:12]) < TOL_ACHIEVED
+
+
 @pytest.mark.parametrize("N", [10, 16, 20, 24, 32])
 def test_reference_golden_fixtures(N):
     """u* of QPs built by the reference's own functions (tests/golden/make_golden.py):

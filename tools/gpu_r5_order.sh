@@ -1,0 +1,30 @@
+#!/bin/bash
+# Round 5: dispatch order (mpcqp_set_order) A/B -- GPU suite, then bench lines of configs 2-5
+# with --order 0 / 1 (two repetitions), and variant libraries (args) with --order 1 on configs 2-3
+#   gpurun -- 'TAG=r5_order bash tools/gpu_r5_order.sh [tools/libX.so ...]'
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+TAG=${TAG:?set TAG}
+O=gpurun_out/$TAG
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; tail -3 $O/tests.log
+if [ $rc -ne 0 ]; then echo "pytest rc $rc: stopping"; grep -E "FAIL|Error" $O/tests.log | head; exit $rc; fi
+line() { python -c 'import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print("%.3f MQP/s kernel %.4f ms frac %s iters %.1f/%d" % (d["value"]/1e6, d["kernel_ms_avg"], d["roofline"]["frac"], d["iters_mean"], d["iters_max"]))'; }
+for rep in 1 2; do
+  for c in config2 config3 config4 config5; do
+    steps=100; [ $c = config5 ] && steps=30
+    for o in 0 1; do
+      out=$(timeout -k 10 180 python bench.py --no-cpu --no-callers --no-hint-line --config $c --steps $steps --warmup 5 --order $o) || exit 1
+      echo "default order=$o $c $(echo "$out" | line)" | tee -a $O/ab_order.txt
+    done
+  done
+  for lib in "$@"; do
+    for c in config2 config3; do
+      out=$(MPCQP_LIB=$lib timeout -k 10 180 python bench.py --no-cpu --no-callers --no-hint-line --config $c --steps 100 --warmup 5 --order 1) || exit 1
+      echo "$lib order=1 $c $(echo "$out" | line)" | tee -a $O/ab_order.txt
+    done
+  done
+done
+timeout -k 10 200 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver_cmd.json || exit $?
+echo "driver cmd $(cat $O/bench_driver_cmd.json | line)"

@@ -27,7 +27,11 @@ def rows(pattern):
 
 
 def kname(name):
-    return "mpcqp_kernel_128" if "kernel_128" in name else ("mpcqp_kernel_64" if "kernel_64" in name else name)
+    for k in ("mpcqp_kernel_128", "mpcqp_kernel_96", "mpcqp_kernel_64", "mpcqp_kernel_ipm", "mpcqp_order_kernel",
+              "mpcqp_plan_kernel", "mpcqp_stance_torque_kernel"):
+        if k in name:
+            return k
+    return name
 
 
 def counter(run_dir, name, kernel):

@@ -12,7 +12,8 @@ for f in glob.glob(out + "/**/*counter_collection.csv", recursive=True):
             k = row.get("Kernel_Name", "")
             if "mpcqp" not in k:
                 continue
-            name = "k64" if "kernel_64" in k else ("k128" if "kernel_128" in k else k[:40])
+            name = next((t for t, key in (("k64", "kernel_64"), ("k96", "kernel_96"), ("k128", "kernel_128"),
+                                          ("kipm", "kernel_ipm"), ("order", "order_kernel")) if key in k), k[:40])
             acc[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
 for name, d in acc.items():
     print(name)
