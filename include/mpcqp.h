@@ -138,12 +138,12 @@ int mpcqp_set_stance_hint(mpcqp_ctx* ctx, int32_t max_stance);
 int mpcqp_set_stance_range(mpcqp_ctx* ctx, int32_t min_stance, int32_t max_stance);
 
 /* Dispatch order (ABI 6; the reference solves one robot at a time and has no batch order).
- * mode 1 (the default): each launch's robots are dealt to workgroups largest predicted solve
- * time first -- the key is the robot's horizontal velocity error |v0 - vref_0|, which tracks
- * its active-set size -- so that a batch queueing on the CUs starts its longest robots first
- * and a batch that fits the chip at once puts its heaviest robots on different CUs.  Costs one
- * small sort launch per solve (batches >= 64 robots whose first class is a dense one); the
- * results are bitwise those of mode 0 (batch order: robot b on workgroup b).
+ * mode 1 (the default): when a batch queues on the CUs (more robots than its first capacity
+ * class holds on the device at once: 4 per CU for class 64, 1 for classes 96 / 128), its
+ * robots are dealt to workgroups largest predicted solve time first -- the key is the robot's
+ * horizontal velocity error |v0 - vref_0|, which tracks its active-set size -- so the longest
+ * robots start first and the launch ends near its mean load.  Costs one small sort launch per
+ * such solve; the results are bitwise those of mode 0 (batch order: robot b on workgroup b).
  * MPCQP_ERR_ARG for any other mode. */
 int mpcqp_set_order(mpcqp_ctx* ctx, int32_t mode);
 

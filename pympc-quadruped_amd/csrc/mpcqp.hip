@@ -61,15 +61,6 @@ static_assert(MPCQP_WARM_BYTES == 4 * kMaxN, "warm-start memory: one byte per (s
 #define MPCQP_CURKEY_MAX_NV 96   // row choice in the current projected metric up to this class (DESIGN 4.1;
                                  // class 96 since its early choice: config 4 +1.5 %)
 #endif
-#ifndef MPCQP_PRIO_T
-#define MPCQP_PRIO_T 0   // A/B only: class 64 raises its waves' issue priority after T, 2T, 3T iterations
-#endif
-#ifndef MPCQP_PRIO_V
-#define MPCQP_PRIO_V 0   // A/B only: class 64's issue priority from its start's violated-row count (>= V, V + 4, V + 8)
-#endif
-#ifndef MPCQP_PRIO_F
-#define MPCQP_PRIO_F 0   // A/B only: class 64's issue priority from the robot's velocity error (1: three bins, 2: one)
-#endif
 #ifndef MPCQP_ASM_COMBO
 // class 64's z / r column combination as one computed jump (mpcqp_combo_asm.h) instead of
 // the compiler's branch tree over an 8-way switch
@@ -362,11 +353,10 @@ __device__ __forceinline__ int xcd_robot(int bid, int B) {
 // time -- grows with the horizontal velocity correction its cone forces must supply: on the
 // benchmark batches |v0 - vref_0| has correlation 0.87 (config 2) / 0.85 (config 4) with the
 // iteration count (tools/order_sim.py).  mpcqp_order_kernel sorts each dispatch segment by
-// that key, largest first, so that (a) in a batch that queues on the CUs (configs 3 to 5) the
-// longest robots start first and the launch ends near its mean load instead of behind a late
-// long robot, and (b) in a batch that fits the chip at once (config 2) the heaviest robots are
-// the first ones dealt to each CU -- one per CU -- instead of meeting on a CU by chance.  Only
-// the robot -> workgroup map changes: every robot's solve is bitwise the same.
+// that key, largest first, so that in a batch that queues on the CUs (configs 3 to 5) the longest
+// robots start first and the launch ends near its mean load instead of behind a late long
+// robot (configs 3 / 4 / 5 +7.7 / +6.2 / +3.7 %, profiles/r5_combo/ab_order.txt).  Only the
+// robot -> workgroup map changes: every robot's solve is bitwise the same.
 constexpr int kOrderMax = 8192;   // robots per sorted segment (one workgroup, 64 KB of LDS)
 constexpr int kOrderMin = 64;     // smaller batches keep their order (nothing to balance)
 
@@ -865,7 +855,12 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   // the dispatch order (mpcqp_order_kernel) of the first class's launch: class 64 sorts its 8 XCD
   // ranges (each <= kOrderMax robots), classes 96 / 128 taking the batch directly sort segments
   // of kOrderMax; the interior-point class and small batches keep the batch order
-  const bool use_order = ctx->order && batch >= kOrderMin && first < 3 && (first > 0 || batch <= 8 * kOrderMax);
+  // -- only when the batch queues on the CUs: a batch the chip holds at once (config 2: 1024
+  // robots = 4 per CU) gains nothing from its order (the heaviest robots' CU-mates are lighter
+  // either way, measured) and would pay the sort launch (config 2 -1.5 %, profiles/r5_combo/)
+  const int resident = (first == 0 ? 4 : 1) * ctx->ncu;   // class 64: 4 workgroups per CU; 96 / 128: 1
+  const bool use_order = ctx->order && batch >= kOrderMin && batch > resident && first < 3 &&
+                         (first > 0 || batch <= 8 * kOrderMax);
   int* q = nullptr;
   QueueSet* qs = nullptr;
   int cap = 0;

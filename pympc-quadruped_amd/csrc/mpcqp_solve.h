@@ -59,7 +59,7 @@ struct alignas(16) SharedT {
 #endif
   union {
     FormArea<NV> fa;
-    double ht[NV * NV];   // element e of thread t at ht[e * NT + t]
+    double ht[NV * NV];   // elements (e, e + 1) of thread t (e even) as one 16-B pair at ht[e * NT + 2 t]
   };
   RobotMeta mt;
   union {
@@ -229,24 +229,6 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   }
   if (wave == 0) form_stance(smf, sm.mt, N, lane);
   fsync<NT>();
-#if MPCQP_PRIO_F > 0
-  // A/B: issue priority from the robot's horizontal velocity error |v0 - vref_0| (its QP's
-  // active set grows with the correction the cone must supply: corr 0.87 with the iteration
-  // count on config 2), so a likely-long robot is not slowed by the robots sharing its SIMDs
-  if constexpr (NV == 64) {
-    using FT = std::remove_reference_t<decltype(smf)>;
-    const float ex = smf.in[IN_X0 + 9] - smf.in[FT::IN_XREF + 9];
-    const float ey = smf.in[IN_X0 + 10] - smf.in[FT::IN_XREF + 10];
-    const float e2 = ex * ex + ey * ey;
-    if (MPCQP_PRIO_F == 1) {
-      if (e2 >= 1.8f * 1.8f) __builtin_amdgcn_s_setprio(3);
-      else if (e2 >= 1.4f * 1.4f) __builtin_amdgcn_s_setprio(2);
-      else if (e2 >= 1.0f * 1.0f) __builtin_amdgcn_s_setprio(1);
-    } else {
-      if (e2 >= 1.4f * 1.4f) __builtin_amdgcn_s_setprio(1);
-    }
-  }
-#endif
   const int S = uni(sm.mt.S);
   const int n = 3 * S, m = 6 * S;
   if (n > NV) {
@@ -319,7 +301,8 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int c = 0; c < TW; ++c) sm.ht[(TW * r + c) * NT + tid] = W[r][c];
+    for (int c = 0; c < TW; c += 2)   // column pairs, lane-interleaved: 16-B accesses
+      reinterpret_cast<d2*>(sm.ht)[((TW * r + c) >> 1) * NT + tid] = d2{W[r][c], W[r][c + 1]};
   STAMP(2);
 
   // ------------------------------------------------ W = H^-1 (symmetric sweep)
@@ -564,19 +547,6 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     u[k] = 0.0;
   }
   if (tid == 0) sm.choice = 0;   // no pass tag yet (MPCQP_SPLIT_CHOICE)
-#if MPCQP_PRIO_V > 0
-  // A/B: a robot whose start violates many rows (a predictor of a long active set, corr 0.78
-  // with the iteration count on config 2) takes issue priority over its SIMD partners
-  if constexpr (NV == 64) {
-    int nv = 0;
-#pragma unroll
-    for (int k = 0; k < CPL; ++k) nv += __popcll(__ballot(s[k] < -1e-9));
-    nv = uni(nv);
-    if (nv >= MPCQP_PRIO_V + 8) __builtin_amdgcn_s_setprio(3);
-    else if (nv >= MPCQP_PRIO_V + 4) __builtin_amdgcn_s_setprio(2);
-    else if (nv >= MPCQP_PRIO_V) __builtin_amdgcn_s_setprio(1);
-  }
-#endif
   // the cone rows' coefficients (lanes 0..17: row r's a_i at 3 r + i) and dependency
   // thresholds 1e-12 |a_r|^2 wscale (lanes 18..23) in one register, read by v_readlane into
   // SGPRs when a row is chosen (an LDS load + readfirstlane chain otherwise)
@@ -708,9 +678,6 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   };
-#if MPCQP_PRIO_T > 0
-  int prio_ = 0;
-#endif
   bool early = false;   // kEarly: wave 1 already holds (and has published) the next choice
   int epc = -1, epc2 = -1;
   SEC(0);
@@ -798,15 +765,6 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       status = MPCQP_STATUS_MAX_ITER;
       break;
     }
-#if MPCQP_PRIO_T > 0
-    // a robot still iterating past T, 2T, 3T iterations takes issue priority over the
-    // younger-in-iterations robots sharing its SIMDs (the launch is its slowest robot)
-    if constexpr (NV == 64) {
-      if (it >= MPCQP_PRIO_T && prio_ < 1) { __builtin_amdgcn_s_setprio(1); prio_ = 1; }
-      if (it >= 2 * MPCQP_PRIO_T && prio_ < 2) { __builtin_amdgcn_s_setprio(2); prio_ = 2; }
-      if (it >= 3 * MPCQP_PRIO_T && prio_ < 3) { __builtin_amdgcn_s_setprio(3); prio_ = 3; }
-    }
-#endif
     SEC(1);
     // z = P a_p, r = R a_p: rows 4tr..4tr+3 in the lanes of tile column tcA
     // (R rows of slots no wave member holds active are zero: skipped)
@@ -1115,11 +1073,13 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     } else {
       // drop slot l: eta = Minv_ll, y = Minv[:, l] = R (H R_l^T)
       const int lt = l >> 2, lr = l & 3;
-      if (tr == lt) {
-        double row[TW];
-#pragma unroll
-        for (int c = 0; c < TW; ++c) row[c] = lr == 0 ? Rm[0][c] : lr == 1 ? Rm[1][c] : lr == 2 ? Rm[2][c] : Rm[3][c];
-        stt<TW>(sm.rl, tc, row);
+      if (tr == lt) {   // lr is wave-uniform: one scalar dispatch, then whole-row stores
+        switch (lr) {
+          case 0: stt<TW>(sm.rl, tc, Rm[0]); break;
+          case 1: stt<TW>(sm.rl, tc, Rm[1]); break;
+          case 2: stt<TW>(sm.rl, tc, Rm[2]); break;
+          default: stt<TW>(sm.rl, tc, Rm[3]); break;
+        }
       }
       fsync<NT>();
       ldt<TW>(cv, sm.rl, tc);
@@ -1131,8 +1091,9 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
           double a = 0.0, a2 = 0.0;
 #pragma unroll
           for (int c = 0; c < TW; c += 2) {
-            a = fma(sm.ht[(TW * r + c) * NT + tid], cv[c], a);
-            a2 = fma(sm.ht[(TW * r + c + 1) * NT + tid], cv[c + 1], a2);
+            const d2 hp = reinterpret_cast<const d2*>(sm.ht)[((TW * r + c) >> 1) * NT + tid];
+            a = fma(hp[0], cv[c], a);
+            a2 = fma(hp[1], cv[c + 1], a2);
           }
           acc[r] = a + a2;
         }
@@ -1153,7 +1114,9 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         aW[r] = rl4[r] * ie;     // P += R_l^T R_l / eta
-        aR[r] = -yv4[r] * ie;    // R -= y R_l / eta
+        // R -= y R_l / eta; row l itself takes exactly -1 (y_l = eta): fma(-1, R_l, R_l) clears
+        // it exactly, with no separate zeroing pass
+        aR[r] = 4 * tr + r == l ? -1.0 : -yv4[r] * ie;
       }
       zrow = l;
       CNT(14);
@@ -1178,16 +1141,6 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         for (int k = 0; k < CPL; ++k) {   // q_c += (a_c . R_l)^2 / eta (sm.rl holds R_l until the next drop)
           const double ar = cdot(sm.rl, k);
           qm[k] = (float)fma(ar * ar, iedrop, (double)qm[k]);
-        }
-      }
-      if (tr == (zrow >> 2)) {   // clear row l of R exactly
-        const int lr = zrow & 3;
-#pragma unroll
-        for (int c = 0; c < TW; ++c) {
-          if (lr == 0) Rm[0][c] = 0.0;
-          if (lr == 1) Rm[1][c] = 0.0;
-          if (lr == 2) Rm[2][c] = 0.0;
-          if (lr == 3) Rm[3][c] = 0.0;
         }
       }
       fsync<NT>();   // the drop buffers are rewritten by the next drop

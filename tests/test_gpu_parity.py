@@ -58,7 +58,7 @@ def test_u0_matches_oracle(N, gaits, robots, tilt):
 
 
 @pytest.mark.parametrize("N,B,gaits,robots,tilt,first", [
-    (10, 1024, ("trot10",), ("a1",), 0.0, 0),                                    # config 2: one launch of class 64
+    (10, 1024, ("trot10",), ("a1",), 0.0, 0),                                    # config 2: held at once, no sort
     (10, 3000, ("trot10", "pace10", "bound8"), ("a1", "aliengo"), 0.0, 0),       # queued class 64, uneven XCD ranges
     (16, 700, ("trot10", "pace10", "bound8"), ("a1",), 0.0, 1),                  # class 96 taking the batch directly
     (20, 300, ("trot10", "pace10", "bound8"), ("a1", "aliengo"), 15.0, 2),       # class 128 directly

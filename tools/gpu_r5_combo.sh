@@ -25,5 +25,6 @@ for rep in 1 2; do
   done
 done
 REPS=2 timeout -k 10 600 bash tools/gpu_ab2.sh default:config4s tools/lib_ipm_mfma_nowpe.so:config4s tools/lib_ipm_base.so:config4s 2>&1 | grep -v amdgpu.ids | tee $O/ab_ipm.txt
+CONFIGS="config2 config3 config4" timeout -k 10 600 bash tools/gpu_ab.sh tools/lib_drop.so 2>&1 | grep -v amdgpu.ids | tee $O/ab_drop.txt
 timeout -k 10 200 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver_cmd.json || exit $?
 echo "driver cmd $(cat $O/bench_driver_cmd.json | line)"
