@@ -77,6 +77,12 @@ static_assert(MPCQP_WARM_BYTES == 4 * kMaxN, "warm-start memory: one byte per (s
 // row values, before its rank-1 / rank-2 FMAs, so wave 0 finds the choice published
 #define MPCQP_EARLY_CHOICE 1
 #endif
+#ifndef MPCQP_SOLO_LDS
+// diagnostic builds only (tools/solo_stamps.py): extra dynamic LDS per class-64 workgroup, so
+// that one robot holds a CU alone -- each robot's solo latency, against the same robot's four
+// robots per CU of the shipped launch
+#define MPCQP_SOLO_LDS 0
+#endif
 // staged inputs (floats)
 constexpr int IN_X0 = 0, IN_FEET = 13, IN_ROBOT = 25, IN_CONTACT = 44;   // + FormT<NM>::IN_XREF
 
@@ -357,8 +363,10 @@ __device__ __forceinline__ int xcd_robot(int bid, int B) {
 // robots start first and the launch ends near its mean load instead of behind a late long
 // robot (configs 3 / 4 / 5 +7.7 / +6.2 / +3.7 %, profiles/r5_combo/ab_order.txt).  Only the
 // robot -> workgroup map changes: every robot's solve is bitwise the same.
-constexpr int kOrderMax = 8192;   // robots per sorted segment (one workgroup, 64 KB of LDS)
+constexpr int kOrderMax = 8192;   // class 64: robots per XCD range the order kernel takes (8 per thread)
+constexpr int kOrderSeg = 1024;   // classes 96 / 128: robots per interleaved segment (one per thread)
 constexpr int kOrderMin = 64;     // smaller batches keep their order (nothing to balance)
+constexpr int kOrderBuckets = 256;
 
 __device__ __forceinline__ float order_key(const float* __restrict__ x0g, const float* __restrict__ xrefg, int N,
                                            int r) {
@@ -368,48 +376,87 @@ __device__ __forceinline__ float order_key(const float* __restrict__ x0g, const 
   return k >= 0.0f && k <= 3.0e38f ? k : 0.0f;   // NaN / inf: no preference
 }
 
-// One workgroup per segment.  mode 0: segment x = class 64's XCD range x (xcd_robot: the robots
-// of blocks x, x + 8, ...), so a sorted range keeps its robots on their XCD's L2; mode 1:
-// consecutive segments of kOrderMax robots (the direct launches of classes 96 / 128, one robot
-// per CU at a time).  perm[lo + j] = the robot of the segment with the j-th largest key (ties:
-// lower index first).
+// One 1024-thread workgroup per segment, a counting sort into 256 key buckets, largest first
+// (the order within a bucket is the atomics' order: it is a schedule, not a result).  A segment
+// is the robots start + stride j (j < len), and rank r goes to position start + stride r:
+//   mode 0: the 8 contiguous XCD ranges of class 64 (xcd_robot: the robots of blocks x, x + 8,
+//           ...), so a sorted range keeps its robots on their XCD's L2;
+//   mode 1: ceil(B / 1024) interleaved segments (stride = their count) for classes 96 / 128
+//           taking the batch directly: position s + S r holds segment s's r-th heaviest robot,
+//           so the workgroups dispatched first get the heaviest robots of every segment.
+// Buckets: sqrt(key / max key) in 256 steps (|v0 - vref_0| relative to the batch's largest).
 __global__ __launch_bounds__(1024) void mpcqp_order_kernel(int B, int N, const float* __restrict__ x0g,
                                                            const float* __restrict__ xrefg, int* __restrict__ perm,
                                                            int mode) {
-  __shared__ unsigned long long key[kOrderMax];
-  const int seg = blockIdx.x, tid = threadIdx.x;
-  int lo, len;
+  __shared__ int hist[kOrderBuckets], cursor[kOrderBuckets];
+  __shared__ unsigned kmax_bits;
+  __shared__ int wsum[kOrderBuckets / LANES];
+  const int seg = blockIdx.x, tid = threadIdx.x, lane = tid & (LANES - 1);
+  int start, stride, len;
   if (mode == 0) {
     const int q = B >> 3, r = B & 7;
-    lo = seg * q + (seg < r ? seg : r);
+    start = seg * q + (seg < r ? seg : r);
+    stride = 1;
     len = q + (seg < r ? 1 : 0);
   } else {
-    lo = seg * kOrderMax;
-    len = B - lo < kOrderMax ? B - lo : kOrderMax;
+    const int S = (B + kOrderSeg - 1) / kOrderSeg;
+    start = seg;
+    stride = S;
+    len = (B - seg + S - 1) / S;
   }
-  if (len <= 0) return;
-  int P = 1;
-  while (P < len) P <<= 1;
-  // (key bits, ~index): non-negative float keys order as their bit patterns; pads are 0 (last)
-  for (int j = tid; j < P; j += 1024)
-    key[j] = j < len ? ((unsigned long long)__float_as_uint(order_key(x0g, xrefg, N, lo + j)) << 32) |
-                           (unsigned long long)(0xffffffffu - (unsigned)j)
-                     : 0ull;
+  constexpr int KPT = kOrderMax / 1024;   // keys per thread
+  float key[KPT];
+  float kmx = 0.0f;
+#pragma unroll
+  for (int t = 0; t < KPT; ++t) {
+    const int j = tid + 1024 * t;
+    key[t] = j < len ? order_key(x0g, xrefg, N, start + stride * j) : 0.0f;
+    kmx = fmaxf(kmx, key[t]);
+  }
+  if (tid < kOrderBuckets) hist[tid] = cursor[tid] = 0;
+  if (tid == 0) kmax_bits = 0u;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) kmx = fmaxf(kmx, __shfl_xor(kmx, o));
   __syncthreads();
-  for (int k = 2; k <= P; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int t = tid; t < (P >> 1); t += 1024) {
-        const int i = 2 * j * (t / j) + (t % j), l = i + j;
-        const unsigned long long a = key[i], c = key[l];
-        if ((a < c) == ((i & k) == 0)) {   // bitonic merge, descending overall
-          key[i] = c;
-          key[l] = a;
-        }
-      }
-      __syncthreads();
+  if (lane == 0) atomicMax(&kmax_bits, __float_as_uint(kmx));   // non-negative floats order as bits
+  __syncthreads();
+  const float inv = kmax_bits ? 1.0f / __uint_as_float(kmax_bits) : 0.0f;
+  int bk[KPT];
+#pragma unroll
+  for (int t = 0; t < KPT; ++t) {
+    const int j = tid + 1024 * t;
+    const int b = min(kOrderBuckets - 1, (int)((float)kOrderBuckets * sqrtf(key[t] * inv)));
+    bk[t] = kOrderBuckets - 1 - b;   // descending: the largest keys first
+    if (j < len) atomicAdd(&hist[bk[t]], 1);
+  }
+  __syncthreads();
+  // exclusive scan of the 256 bucket counts (4 waves)
+  if (tid < kOrderBuckets) {
+    const int v = hist[tid];
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < LANES; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == LANES - 1) wsum[tid >> 6] = x;
+    hist[tid] = x - v;   // exclusive within the wave
+  }
+  __syncthreads();
+  if (tid < kOrderBuckets) {
+    int off = 0;
+    for (int w = 0; w < (tid >> 6); ++w) off += wsum[w];
+    hist[tid] += off;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < KPT; ++t) {
+    const int j = tid + 1024 * t;
+    if (j < len) {
+      const int pos = hist[bk[t]] + atomicAdd(&cursor[bk[t]], 1);
+      perm[start + stride * pos] = start + stride * j;
     }
   }
-  for (int j = tid; j < len; j += 1024) perm[lo + j] = lo + (int)(0xffffffffu - (unsigned)(key[j] & 0xffffffffull));
 }
 
 // class 64's capacity (stance variables)
@@ -853,8 +900,8 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   // standing robots only as its own workgroups run, and the fork would wait for all of it.
   const int first = ipm_only || nmin > 128 ? 3 : giant ? 0 : nmin > 96 ? 2 : nmin > kCap64 ? 1 : 0;
   // the dispatch order (mpcqp_order_kernel) of the first class's launch: class 64 sorts its 8 XCD
-  // ranges (each <= kOrderMax robots), classes 96 / 128 taking the batch directly sort segments
-  // of kOrderMax; the interior-point class and small batches keep the batch order
+  // ranges (each <= kOrderMax robots), classes 96 / 128 taking the batch directly sort interleaved
+  // segments of <= kOrderSeg; the interior-point class and small batches keep the batch order
   // -- only when the batch queues on the CUs: a batch the chip holds at once (config 2: 1024
   // robots = 4 per CU) gains nothing from its order (the heaviest robots' CU-mates are lighter
   // either way, measured) and would pay the sort launch (config 2 -1.5 %, profiles/r5_combo/)
@@ -935,14 +982,15 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
     return code;
   };
   if (use_order) {
-    const int segs = first == 0 ? 8 : (int)((batch + kOrderMax - 1) / kOrderMax);
+    const int segs = first == 0 ? 8 : (int)((batch + kOrderSeg - 1) / kOrderSeg);
     hipLaunchKernelGGL(mpcqp_order_kernel, dim3(segs), dim3(1024), 0, st, (int)batch, kp.N, x0, xref, perm,
                        first == 0 ? 0 : 1);
     e = hipGetLastError();
     if (e != hipSuccess) return failed(set_err(ctx, MPCQP_ERR_HIP, std::string("launch (order): ") + hipGetErrorString(e)));
   }
   if (first == 0) {
-    hipLaunchKernelGGL(full ? mpcqp_kernel_64<true> : mpcqp_kernel_64<false>, dim3(batch), dim3(Cfg<64>::NT), 0, st, kp, (int)batch, x0, xref, contact,
+    hipLaunchKernelGGL(full ? mpcqp_kernel_64<true> : mpcqp_kernel_64<false>, dim3(batch), dim3(Cfg<64>::NT),
+                       MPCQP_SOLO_LDS, st, kp, (int)batch, x0, xref, contact,
                        feet, robot, u0, U, (int*)status, (int*)iters, q1, q2, q3, perm);
     e = hipGetLastError();
     if (e != hipSuccess) return failed(set_err(ctx, MPCQP_ERR_HIP, std::string("launch: ") + hipGetErrorString(e)));
