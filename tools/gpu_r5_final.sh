@@ -39,7 +39,10 @@ PY
 else
 for c in config2 config3 config4 config5; do
   bash tools/profile.sh $TAG --config $c > $O/profile_$c.log 2>&1 || { tail -20 $O/profile_$c.log; exit 1; }
+  cp gpurun_out/prof_$TAG/summary/kt_kernel_stats.csv $O/kt_${c}_kernel_stats.csv
+  cp gpurun_out/prof_$TAG/bench_kt.json $O/bench_kt_$c.json
 done
+[ -n "$PROFILE_ONLY" ] && { echo done; exit 0; }
 timeout -k 10 150 python3 tools/phase_stamps.py 1024 10 trot10 > $O/stamps_c2.txt 2>&1 || exit $?
 timeout -k 10 200 python3 tools/phase_stamps.py 2048 16 trot10,pace10,bound8 > $O/stamps_c4_class96.txt 2>&1 || exit $?
 timeout -k 10 300 python3 tools/phase_stamps.py 8192 20 trot10,pace10,bound8 > $O/stamps_c5_class128.txt 2>&1 || exit $?
