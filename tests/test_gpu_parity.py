@@ -85,6 +85,33 @@ def test_dispatch_order_is_bitwise_neutral(N, B, gaits, robots, tilt, first):
     assert rel_err_u0(out[1][0][B - 1], x[:12]) < TOL_ACHIEVED
 
 
+def test_dispatch_order_nonfinite_and_tied_keys():
+    """The order kernel's key guards: non-finite states (key 0, dealt last; the robots
+    report MPCQP_STATUS_NONFINITE) and a batch whose keys are all zero (v0 = vref_0: every
+    robot in one bucket) keep the batch-order results bitwise."""
+    from mpcqp.synthetic import make_batch
+    N, B = 10, 3000
+    bt = make_batch(B, N, seed=77, gaits=("trot10",), robots=("a1",))
+    bt["x0"][7, 9] = np.nan
+    bt["x0"][11, 10] = np.inf
+    bt["x0"][13, 9] = 3e38   # finite: the batch's largest key
+    tied = {k: v.copy() for k, v in bt.items()}
+    xr = tied["xref"].reshape(B, N, 13)
+    tied["x0"][:, 9:11] = xr[:, 0, 9:11]
+    for batch in (bt, tied):
+        out = []
+        for mode in (0, 1):
+            eng = _engine(N)
+            eng.set_order(mode)
+            out.append(_solve(eng, batch))
+        for a, b in zip(out[0], out[1]):
+            assert np.array_equal(a, b)
+    st = out[1][2]
+    assert (st == 0).all()   # the tied batch
+    st = _solve(_engine(N), bt)[2]
+    assert st[7] == 4 and st[11] == 4, (st[7], st[11])
+
+
 @pytest.mark.parametrize("N", [10, 16, 20, 24, 32])
 def test_reference_golden_fixtures(N):
     """u* of QPs built by the reference's own functions (tests/golden/make_golden.py):
