@@ -649,6 +649,29 @@ def test_full_weights_match_oracle(N):
         np.testing.assert_array_equal(a, c)
 
 
+@pytest.mark.parametrize("N,B,first", [(10, 3000, False), (16, 600, True), (20, 300, True)])
+def test_dispatch_order_full_weights(N, B, first):
+    """The full-weight kernel instantiations (mpcqp_set_weights) under the dispatch order:
+    class 64 sorting its XCD ranges, classes 96 / 128 taking the batch directly -- bitwise
+    equal to batch order, and on the oracle's optimum."""
+    from mpcqp.synthetic import make_batch
+    bt = make_batch(B, N, seed=950 + N, gaits=("trot10", "pace10", "bound8"), robots=("a1",))
+    stance = (bt["contact"] > 0).reshape(B, -1).sum(1)
+    Q, R = _full_weights(N)
+    out = []
+    for mode in (0, 1):
+        eng = _engine(N, Q=Q, R=R)
+        if first:
+            eng.set_stance_range(int(stance.min()), int(stance.max()))
+        eng.set_order(mode)
+        out.append(_solve(eng, bt))
+    for a, b in zip(out[0], out[1]):
+        assert np.array_equal(a, b)
+    assert (out[1][2] == 0).all()
+    x, _, _ = oracle_solution(bt, B - 1, N, Q=Q, R=R)
+    assert rel_err_u0(out[1][0][B - 1], x[:12]) < TOL_U0
+
+
 def test_full_weights_cross_leg_r_and_validation():
     """A cross-leg R entry: the dense classes solve it (oracle parity); the
     interior-point class, whose Riccati stages are per leg, reports
