@@ -112,6 +112,29 @@ def test_dispatch_order_nonfinite_and_tied_keys():
     assert st[7] == 4 and st[11] == 4, (st[7], st[11])
 
 
+def test_dispatch_order_batch_limits():
+    """Class 64 sorts each XCD's range only up to kOrderMax = 8192 robots per range (a batch
+    above 65 536 keeps the batch order) and never below kOrderMin = 64 or when the chip
+    holds the batch at once: both sides of the upper limit, with the order on and off,
+    give the same solutions."""
+    from mpcqp.synthetic import make_batch
+    N = 10
+    full = make_batch(65544, N, seed=31, gaits=("trot10", "pace10"), robots=("a1",))
+    for B in (65536, 65544):
+        bt = {k: v[:B] for k, v in full.items()}
+        out = []
+        for mode in (0, 1):
+            eng = _engine(N)
+            eng.set_order(mode)
+            out.append(_solve(eng, bt))
+        for a, b in zip(out[0], out[1]):
+            assert np.array_equal(a, b)
+        assert (out[1][2] == 0).all()
+        for b in (0, B // 3, B - 1):
+            x, _, _ = oracle_solution(bt, b, N)
+            assert rel_err_u0(out[1][0][b], x[:12]) < TOL_U0, (B, b)
+
+
 @pytest.mark.parametrize("N", [10, 16, 20, 24, 32])
 def test_reference_golden_fixtures(N):
     """u* of QPs built by the reference's own functions (tests/golden/make_golden.py):
