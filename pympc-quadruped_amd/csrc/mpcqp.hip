@@ -47,42 +47,6 @@ constexpr int kDenseN = 20;   // the dense classes' LDS layouts hold N <= 20; lo
                               // the interior-point class, sized for N <= kMaxN
 static_assert(kMaxN >= kDenseN && 4 * kMaxN <= 2 * LANES, "stance lists cover 4 N <= 128 entries");
 static_assert(MPCQP_WARM_BYTES == 4 * kMaxN, "warm-start memory: one byte per (stage, leg)");
-#ifndef MPCQP_SPLIT_CHOICE
-#define MPCQP_SPLIT_CHOICE 1   // class 64: wave 1 chooses the next rows, wave 0 reads them; 0: both choose
-#endif
-#ifndef MPCQP_SPLIT96
-#define MPCQP_SPLIT96 1   // class 96: wave 1 chooses, the other five waves read its published choice (+1.2 %)
-#endif
-
-#ifndef MPCQP_PAIR_MAX_NV
-#define MPCQP_PAIR_MAX_NV 96   // pair steps in classes 64 and 96 (class 128: no VGPRs to spare)
-#endif
-#ifndef MPCQP_CURKEY_MAX_NV
-#define MPCQP_CURKEY_MAX_NV 96   // row choice in the current projected metric up to this class (DESIGN 4.1;
-                                 // class 96 since its early choice: config 4 +1.5 %)
-#endif
-#ifndef MPCQP_ASM_COMBO
-// class 64's z / r column combination as one computed jump (mpcqp_combo_asm.h) instead of
-// the compiler's branch tree over an 8-way switch
-#define MPCQP_ASM_COMBO 1
-#endif
-#ifndef MPCQP_SLOT_COEF
-#define MPCQP_SLOT_COEF 1   // class 64: pair steps' R row coefficients computed once per slot lane
-#endif
-#ifndef MPCQP_F32_KEY
-#define MPCQP_F32_KEY 1   // row keys in f32 throughout (not bitwise identical to f64 keys: near-ties may resolve differently)
-#endif
-#ifndef MPCQP_EARLY_CHOICE
-// class 64 split choice: wave 1 chooses the next rows as soon as the pass has updated the
-// row values, before its rank-1 / rank-2 FMAs, so wave 0 finds the choice published
-#define MPCQP_EARLY_CHOICE 1
-#endif
-#ifndef MPCQP_SOLO_LDS
-// diagnostic builds only (tools/solo_stamps.py): extra dynamic LDS per class-64 workgroup, so
-// that one robot holds a CU alone -- each robot's solo latency, against the same robot's four
-// robots per CU of the shipped launch
-#define MPCQP_SOLO_LDS 0
-#endif
 // staged inputs (floats)
 constexpr int IN_X0 = 0, IN_FEET = 13, IN_ROBOT = 25, IN_CONTACT = 44;   // + FormT<NM>::IN_XREF
 
@@ -123,7 +87,16 @@ struct KParams {
     __builtin_amdgcn_sched_barrier(0);                           \
   } while (0)
 #define CNT(k) (secacc_ += (lane == (k)) ? 1ull : 0ull)
+#ifndef MPCQP_SOLO_LDS
+// stamps builds only (tools/solo_stamps.py): extra dynamic LDS per class-64 workgroup, so that one
+// robot holds a CU alone -- each robot's solo latency against its four robots per CU
+#define MPCQP_SOLO_LDS 0
+#endif
+constexpr unsigned kDiagLds = MPCQP_SOLO_LDS;
+constexpr int kStampU64 = 256;   // stamp slots per robot (the stamps build's U buffer: 512 floats per robot)
+static_assert(32 + 24 * 8 <= kStampU64, "eight waves' section accumulators");
 #else
+constexpr unsigned kDiagLds = 0;
 #define CNT(k) \
   do {         \
   } while (0)
@@ -269,6 +242,22 @@ __device__ __forceinline__ void stt(double* base, int k, const double (&v)[TW]) 
   d2* p = reinterpret_cast<d2*>(base + TW * k);
 #pragma unroll
   for (int i = 0; i < TW / 2; ++i) p[i] = d2{v[2 * i], v[2 * i + 1]};
+}
+// TW consecutive doubles starting at element TS k (TS >= TW: a padded tile-column stride)
+template <int TW, int TS>
+__device__ __forceinline__ void lds_t(double (&v)[TW], const double* base, int k) {
+  const d2* p = reinterpret_cast<const d2*>(base + TS * k);
+#pragma unroll
+  for (int i = 0; i < TW / 2; ++i) {
+    const d2 x = p[i];
+    v[2 * i] = x[0];
+    v[2 * i + 1] = x[1];
+  }
+}
+// 4 consecutive doubles at p (16-B aligned)
+__device__ __forceinline__ void ld4s(double (&v)[4], const double* p) {
+  const d2 a = reinterpret_cast<const d2*>(p)[0], b = reinterpret_cast<const d2*>(p)[1];
+  v[0] = a[0]; v[1] = a[1]; v[2] = b[0]; v[3] = b[1];
 }
 __device__ __forceinline__ void ld4(double (&v)[4], const double* base, int k) {
   const d2* p = reinterpret_cast<const d2*>(base + 4 * k);
@@ -990,7 +979,7 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
   }
   if (first == 0) {
     hipLaunchKernelGGL(full ? mpcqp_kernel_64<true> : mpcqp_kernel_64<false>, dim3(batch), dim3(Cfg<64>::NT),
-                       MPCQP_SOLO_LDS, st, kp, (int)batch, x0, xref, contact,
+                       kDiagLds, st, kp, (int)batch, x0, xref, contact,
                        feet, robot, u0, U, (int*)status, (int*)iters, q1, q2, q3, perm);
     e = hipGetLastError();
     if (e != hipSuccess) return failed(set_err(ctx, MPCQP_ERR_HIP, std::string("launch: ") + hipGetErrorString(e)));

@@ -36,11 +36,9 @@ constexpr int IPM_MAX_IT = 60;
 constexpr int IPM_NCORR = 8;
 constexpr int IPM_NREF = 2;
 constexpr double IPM_TAU = 0.995;
-#ifndef MPCQP_IPM_POLISH_MU
-#define MPCQP_IPM_POLISH_MU 3e-9   // polish once mu < this * scale (tools/ipm_ab.sh: 1e-7 -> 3e-9 cut the
-                                    // slowest of 256 standing robots from 31 to 18 factorisations)
-#endif
-constexpr double IPM_POLISH_MU = MPCQP_IPM_POLISH_MU;
+// polish once mu < this * scale (tools/ipm_ab.sh: 1e-7 -> 3e-9 cut the slowest of 256 standing
+// robots from 31 to 18 factorisations)
+constexpr double IPM_POLISH_MU = 3e-9;
 constexpr double IPM_MU_FLOOR = 1e-13;
 constexpr double IPM_STAT_TOL = 1e-10;
 constexpr int IPM_FPL = 2;             // stance foot-steps per lane (4 kMaxN <= 128)

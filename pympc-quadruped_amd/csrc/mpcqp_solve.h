@@ -36,6 +36,13 @@ struct Cfg {
   static constexpr int CPL = NV / 32;         // constraint rows per lane (m = 6S <= 2NV)
   static constexpr int VPL = (NV + LANES - 1) / LANES;   // variables / slots per lane
   static constexpr int VEC = VPL * LANES;     // LDS vector length (entries >= NV are padding)
+  // The sweep's pivot columns: each tile column's TW-double slice at a stride of TS doubles.
+  // ds_read_b128 serves a wave in four 16-lane groups that each hold every tile column (class
+  // 128) or every one twice (class 64); at a 64-B stride the slices fold onto 4 (2) of the
+  // 256-B bank row's 16 slots, a 4-way (2-way) conflict.  80 B puts the 16 (8) slices on
+  // distinct slots; class 96's 48-B stride already does.
+  static constexpr int TS = TW == 8 ? 10 : TW;
+  static constexpr int SVEC = TW == 8 ? TCN * TS : VEC;   // class 96: the unpadded vectors
   static_assert(NW * LANES * 4 * TW == NV * NV, "4 x TW tiles");
   static_assert(TCN == 8 || TCN == 16, "tile rows are reduced over 8 or 16 lanes");
 };
@@ -52,11 +59,7 @@ struct FormArea {
 };
 template <int NV>
 struct alignas(16) SharedT {
-#ifdef MPCQP_NO_PAIR
-  static constexpr bool kPair = false;
-#else
-  static constexpr bool kPair = NV <= MPCQP_PAIR_MAX_NV;   // class 128 has no VGPRs to spare for pair steps
-#endif
+  static constexpr bool kPair = NV <= 96;   // pair steps in classes 64 / 96 (class 128: no VGPRs to spare)
   union {
     FormArea<NV> fa;
     double ht[NV * NV];   // elements (e, e + 1) of thread t (e even) as one 16-B pair at ht[e * NT + 2 t]
@@ -69,6 +72,9 @@ struct alignas(16) SharedT {
       alignas(16) double vz[2][Cfg<NV>::VEC];   // z = P a_p (double-buffered by iteration)
     };
     double wb[4 * Cfg<NV>::VEC];   // between sweep and loop: W's 3x3 foot-step blocks (9 S <= 4 NV)
+    // the sweep's pivot columns, tile-column stride TS: two (class 64, single pivots) or two
+    // pairs (classes 96 / 128), double-buffered
+    alignas(16) double swz[(NV >= 96 ? 4 : 2) * Cfg<NV>::SVEC];
   };
   alignas(16) double vr[2][Cfg<NV>::VEC];   // r = R a_p (slot-indexed)
   union {
@@ -82,10 +88,11 @@ struct alignas(16) SharedT {
   alignas(16) double tv[Cfg<NV>::VEC];
   alignas(16) double yv[Cfg<NV>::VEC];
   double wmax[Cfg<NV>::NW];
-  int choice;   // class 64, MPCQP_SPLIT_CHOICE: wave 1's published {pass tag, p2 + 1, p + 1}
+  int choice;   // classes 64 / 96 (split choice): wave 1's published {pass tag, p2 + 1, p + 1}
 };
 // the formulation scratch must not grow the H copy's union (class 64: 4 robots per CU)
 static_assert(sizeof(FormArea<64>) <= sizeof(double) * 64 * 64, "formulation scratch exceeds the H copy");
+static_assert(sizeof(SharedT<64>) <= 160 * 1024 / 4, "class 64 holds four robots per CU");
 
 constexpr int DPP_SHL1 = 0x101;   // row_shl:1 -- lane i reads lane i + 1 (same 16-lane row)
 constexpr int DPP_ROR8 = 0x128;   // row_ror:8 -- lane i <-> i ^ 8 inside 16 lanes
@@ -144,29 +151,9 @@ __device__ __forceinline__ double tile_matvec4(const double (&M)[4][TW], const d
   return tile_reduce<TCN>(acc, lane);
 }
 
-// z / r column combination: out[r] = sum_k al_k M[r][(C0 + k) & 7]; the R half
-// only where the wave's slot rows hold an active constraint (rlive, wave-uniform)
-template <int C0, int TW>
-__device__ __forceinline__ void colcombo(const double (&Pm)[4][TW], const double (&Rm)[4][TW], int tc, int tcA,
-                                         double a0, double a1, double a2, bool rlive, double (&zq)[4],
-                                         double (&rq)[4]) {
-  const double al0 = (tc == tcA + (C0 + 0) / TW) ? a0 : 0.0;
-  const double al1 = (tc == tcA + (C0 + 1) / TW) ? a1 : 0.0;
-  const double al2 = (tc == tcA + (C0 + 2) / TW) ? a2 : 0.0;
-  constexpr int c0 = C0 % TW, c1 = (C0 + 1) % TW, c2 = (C0 + 2) % TW;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) zq[r] = fma(al2, Pm[r][c2], fma(al1, Pm[r][c1], al0 * Pm[r][c0]));
-  if (rlive) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) rq[r] = fma(al2, Rm[r][c2], fma(al1, Rm[r][c1], al0 * Rm[r][c0]));
-  } else {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) rq[r] = 0.0;
-  }
-}
-
-// colcombo without the per-lane tile-column mask (uniform coefficients): for foot-steps
-// that lie inside one tile column, whose lanes alone store the result
+// z / r column combination out[r] = a0 M[r][C0] + a1 M[r][C0 + 1] + a2 M[r][C0 + 2] with uniform
+// coefficients (class 96: a foot-step never straddles two tile columns, whose lanes alone store
+// the result); the R half only where the wave's slot rows hold an active constraint (rlive)
 template <int C0, int TW>
 __device__ __forceinline__ void colcombo_u(const double (&Pm)[4][TW], const double (&Rm)[4][TW], double a0, double a1,
                                            double a2, bool rlive, double (&zq)[4], double (&rq)[4]) {
@@ -306,6 +293,8 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   STAMP(2);
 
   // ------------------------------------------------ W = H^-1 (symmetric sweep)
+  // element 4 tr (the lane's tile row) of a pivot column in the strided layout
+  const int i4s = C::TS * (tr >> 1) + 4 * (tr & 1);   // TW = 8
   if constexpr (NV >= 96) {
   // Classes 96 / 128 (one robot per CU, latency-bound; 6- / 8-wave barriers):
   // pivot PAIRS {K, K + 1} (K even: one tile column, one 4-row group; K + 1 = n is
@@ -326,23 +315,31 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       const int KR = TW == 8 ? 2 * KT + (KC >> 2) : K >> 2;
       const int KRR = TW == 8 ? (KC & 3) : (K & 3);   // 0 or 2
       if (K < n) {
-        double* const z0 = sm.zc[0] + ((K >> 1) & 1) * (2 * C::VEC);
-        double* const z1 = z0 + C::VEC;
+        // class 96 keeps its unpadded vectors (zc / vz) and their addressing as it was
+        double* const z0 = (TW == 8 ? sm.swz : sm.zc[0]) + ((K >> 1) & 1) * (2 * C::SVEC);
+        double* const z1 = z0 + C::SVEC;
+        const int ks = TW == 8 ? C::TS * KT + KC : K;   // element K in the strided layout
+        const int i4 = TW == 8 ? i4s : 4 * tr;
         if (tc == KT) {
-          d2* q0 = reinterpret_cast<d2*>(z0 + 4 * tr);
+          d2* q0 = reinterpret_cast<d2*>(z0 + i4);
           q0[0] = d2{W[0][KC], W[1][KC]};
           q0[1] = d2{W[2][KC], W[3][KC]};
-          d2* q1 = reinterpret_cast<d2*>(z1 + 4 * tr);
+          d2* q1 = reinterpret_cast<d2*>(z1 + i4);
           q1[0] = d2{W[0][KC + 1], W[1][KC + 1]};
           q1[1] = d2{W[2][KC + 1], W[3][KC + 1]};
         }
         fsync<NT>();
         double zr0[TW], zr1[TW], zi0[4], zi1[4];
-        ldt<TW>(zr0, z0, tc);
-        ldt<TW>(zr1, z1, tc);
-        ld4(zi0, z0, tr);
-        ld4(zi1, z1, tr);
-        const double d00 = z0[K], d01 = z0[K + 1], d11 = z1[K + 1];
+        lds_t<TW, C::TS>(zr0, z0, tc);
+        lds_t<TW, C::TS>(zr1, z1, tc);
+        if constexpr (TW == 8) {
+          ld4s(zi0, z0 + i4s);
+          ld4s(zi1, z1 + i4s);
+        } else {
+          ld4(zi0, z0, tr);
+          ld4(zi1, z1, tr);
+        }
+        const double d00 = z0[ks], d01 = z0[ks + 1], d11 = z1[ks + 1];
         const double idet = rcp_nr(fma(d00, d11, -d01 * d01));
         const double e00 = d11 * idet, e01 = -d01 * idet, e11 = d00 * idet;   // D^-1
         double c0[4], c1[4];
@@ -407,17 +404,17 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       const int KR = TW == 8 ? 2 * KT + (KC >> 2) : K >> 2;
       const int KRR = TW == 8 ? (KC & 3) : (K & 3);
       if (K < n) {
-        double* const zc = sm.zc[KC & 1];
+        double* const zc = sm.swz + (KC & 1) * C::SVEC;
         if (tc == KT) {
-          d2* pz = reinterpret_cast<d2*>(zc + 4 * tr);
+          d2* pz = reinterpret_cast<d2*>(zc + i4s);
           pz[0] = d2{W[0][KC], W[1][KC]};
           pz[1] = d2{W[2][KC], W[3][KC]};
         }
         fsync<NT>();
         double zr[TW], zi[4];
-        ldt<TW>(zr, zc, tc);
-        ld4(zi, zc, tr);
-        const double dK = zc[K];
+        lds_t<TW, C::TS>(zr, zc, tc);
+        ld4s(zi, zc + i4s);
+        const double dK = zc[C::TS * KT + KC];
         const double inv = rcp_nr(dK);
         double beta[4];
 #pragma unroll
@@ -514,7 +511,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   // class 128 keeps the initial metric: the per-pass updates cost more than the passes they
   // save (config 5 -1 %); class 96 uses the current one since its choosing wave updates q_c
   // in the early-choice block (config 4 +1.5 %; before the early choice -3 %)
-  constexpr bool kCurKey = NV <= MPCQP_CURKEY_MAX_NV;
+  constexpr bool kCurKey = NV <= 96;
   float qm[CPL];   // a_c^T P a_c (f32, classes 64 / 96; class 128: 1 / sqrt(a_c^T W a_c)): scales the f32 row key
   auto cdot = [&](const double* v, int k) -> double {
     const double* a = sm.mt.rows[crt[k]];
@@ -546,7 +543,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     x[k] = sm.vx[lane + LANES * k];
     u[k] = 0.0;
   }
-  if (tid == 0) sm.choice = 0;   // no pass tag yet (MPCQP_SPLIT_CHOICE)
+  if (tid == 0) sm.choice = 0;   // no pass tag yet (split choice)
   // the cone rows' coefficients (lanes 0..17: row r's a_i at 3 r + i) and dependency
   // thresholds 1e-12 |a_r|^2 wscale (lanes 18..23) in one register, read by v_readlane into
   // SGPRs when a row is chosen (an LDS load + readfirstlane chain otherwise)
@@ -589,16 +586,15 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   // LDS word the other waves read (class 96: its six waves sit 2-2-1-1 on the SIMDs, so
   // five fewer argmins free the shared SIMDs' issue: config 4 +1.2 %, bitwise identical)
   // (class 128 would spill: 138 VGPRs with the split choice)
-  constexpr bool kSplit = MPCQP_SPLIT_CHOICE && ((NV == 64 && C::NW == 2) || (NV == 96 && MPCQP_SPLIT96));
+  constexpr bool kSplit = NV <= 96;
   // early choice: the choosing wave (wave 1 of the split choice; the only wave of the one-wave
   // class 64) chooses the next rows before a pass's rank updates, which then overlap it
   // (class 96 with the split choice: config 4 +4.7 %, bitwise identical)
-  constexpr bool kEarly = (NV == 64 || NV == 96) && kSplit && MPCQP_EARLY_CHOICE;
+  constexpr bool kEarly = kSplit;
   constexpr int kChooser = 1;
   auto choose = [&](int tag_it, int& pc, int& pc2) {
     pc = -1;
     pc2 = -1;
-#if MPCQP_F32_KEY
     if constexpr (kCurKey) {   // the keys in f32 throughout: the argmin is an f32 selection anyway
       float keyf[CPL];
 #pragma unroll
@@ -639,11 +635,10 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       }
       return;
     }
-#endif
+    // class 128: f64 keys in the initial metric (qm = 1 / sqrt(a_c^T W a_c))
     double key[CPL];
 #pragma unroll
-    for (int k = 0; k < CPL; ++k)
-      key[k] = s[k] < -tol ? s[k] * (double)(kCurKey ? __builtin_amdgcn_rsqf(fmaxf(qm[k], qfloor)) : qm[k]) : INFINITY;
+    for (int k = 0; k < CPL; ++k) key[k] = s[k] < -tol ? s[k] * (double)qm[k] : INFINITY;
     double bv = key[0];
     int bk = 0;
 #pragma unroll
@@ -688,7 +683,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     if (p < 0) {
       // the next row p (and its pair candidate p2): the most violated row in the dual
       // metric (f32-rounded keys, lowest lane on ties), then the best row of any other
-      // foot-step.  Class 64 with MPCQP_SPLIT_CHOICE: wave 1 -- whose slot rows of R
+      // foot-step.  Classes 64 / 96 (split choice): wave 1 -- whose slot rows of R
       // are idle while <= 32 slots are active -- chooses and publishes {p, p2} in one
       // pass-tagged LDS word, which wave 0 reads after its R update instead of
       // repeating both argmins (every decision is identical in both waves, so both
@@ -771,14 +766,13 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     const bool rlive = slots_live(RPW * wave);
     // rows 4tr..4tr+3 of P a and R a for a row a of the foot-step at variable
     // 8 tA + cA, stored by the lanes of tile column tA
-    constexpr bool kAsmCombo = (NV == 64 || NV == 128) && TW == 8 && MPCQP_ASM_COMBO;
     auto combo_store = [&](int cA, int tA, double e0, double e1, double e2, double* dz, double* dr) {
       double zq[4], rq[4];
       if constexpr (TW == 6) {   // foot-steps start at register column 0 or 3: never straddle,
         // so the uniform (SGPR) coefficients need no per-lane mask: only tile column tA stores
         if (cA == 0) colcombo_u<0, TW>(W, Rm, e0, e1, e2, rlive, zq, rq);
         else colcombo_u<3, TW>(W, Rm, e0, e1, e2, rlive, zq, rq);
-      } else if constexpr (kAsmCombo) {
+      } else {   // TW = 8: classes 64 and 128
         // one computed jump into straight-line cases (mpcqp_combo_asm.h); R's half
         // unconditionally (rows of no active slot are zero; a second, P-only table for those
         // waves measured 0.6 % slower).  A foot-step inside one tile column (c0 <= 5) takes
@@ -795,24 +789,6 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
           }
         } else {
           combo_asm64_s(W, Rm, cA, e0, e1, e2, zq, rq);
-        }
-      } else {
-        switch (cA) {
-          case 0: colcombo<0, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-          case 1: colcombo<1, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-          case 2: colcombo<2, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-          case 3: colcombo<3, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-          case 4: colcombo<4, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-          case 5: colcombo<5, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-          case 6: colcombo<6, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-          default: colcombo<7, TW>(W, Rm, tc, tA, e0, e1, e2, rlive, zq, rq); break;
-        }
-      }
-      if (TW == 8 && !kAsmCombo && __builtin_expect(cA + 2 >= TW, 0)) {   // straddles tile columns tA, tA + 1
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          zq[r] += dpp_shl1(zq[r]);
-          rq[r] += dpp_shl1(rq[r]);
         }
       }
       if (tc == tA) {
@@ -916,7 +892,7 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         // same values), read back by tile row below -- instead of per tile row, with two
         // LDS loads and two selects each (tv / yv are written only on drop passes, after
         // the next pass's barrier)
-        constexpr bool kSlotCoef = NV == 64 && VPL == 1 && MPCQP_SLOT_COEF;
+        constexpr bool kSlotCoef = NV == 64;
         const double i11 = s22 * id, i12 = -s12 * id, i22 = zsp * id;
         if constexpr (kSlotCoef) {
           const double e1 = rs1[0] - (lane == qa ? 1.0 : 0.0);
@@ -1037,11 +1013,8 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       for (int k = VPL - 1; k >= 0; --k)
         if (~occ[k]) q = LANES * k + __builtin_ctzll(~occ[k]);
       const double is = rcp_nr(zsp);
-      if constexpr (kCurKey && !kEarly)
-#pragma unroll
-        for (int k = 0; k < CPL; ++k) qm[k] = (float)fma(-zs[k] * zs[k], is, (double)qm[k]);
       double zr4[4], rr4[4];
-      constexpr bool kSlotCoef1 = NV == 64 && VPL == 1 && MPCQP_SLOT_COEF;
+      constexpr bool kSlotCoef1 = NV == 64;
       if constexpr (kSlotCoef1) {   // R's row coefficient once per slot lane (as the pair step's)
         sm.tv[lane] = ((lane == q) ? 1.0 - rs[0] : -rs[0]) * is;
         fsync<LANES>();
@@ -1175,28 +1148,21 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   STAMP(6);
 
 #ifdef MPCQP_STAMPS
-  if (tid == 0 && Ug) {
-    unsigned long long* dst = (unsigned long long*)(Ug + (size_t)b * N * 12);
-    for (int i = 0; i < 7; ++i) dst[i] = stamps_[i];
-    if (N * 6 > 45) {
-      dst[44] = rt0_;
-      dst[45] = __builtin_amdgcn_s_memrealtime();
+  // stamps build: U is a diagnostic buffer of kStampU64 u64 per robot (tools/phase_stamps.py):
+  // [0, 7) phase stamps, 7 / 8 chip-wide start / end (s_memrealtime), [16, 24) each wave's HW_ID,
+  // [32 + 24 w, 56 + 24 w) wave w's section accumulators and event counters (lane k: section k)
+  if (Ug) {
+    unsigned long long* dst = (unsigned long long*)Ug + (size_t)b * kStampU64;
+    if (tid == 0) {
+      for (int i = 0; i < 7; ++i) dst[i] = stamps_[i];
+      dst[7] = rt0_;
+      dst[8] = __builtin_amdgcn_s_memrealtime();
     }
-  }
-  fsync<NT>();
-  if (lane < 16 && Ug && 26 + 16 * (NT / LANES - 1) < N * 6) {   // per-wave section accumulators
-    unsigned long long* dst = (unsigned long long*)(Ug + (size_t)b * N * 12);
-    dst[(wave == 0 ? 8 : 10 + 16 * wave) + lane] = secacc_;
-  }
-  if (lane >= 16 && lane < 19 && Ug && NT == 128 && N * 6 >= 52) {   // sections 16..18 (pair step split)
-    unsigned long long* dst = (unsigned long long*)(Ug + (size_t)b * N * 12);
-    dst[46 + 3 * wave + (lane - 16)] = secacc_;
-  }
-  if (lane == 0 && Ug && 24 + wave < N * 6) {   // HW_ID of each wave (SIMD, CU, SE)
-    unsigned long long* dst = (unsigned long long*)(Ug + (size_t)b * N * 12);
-    dst[24 + wave] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
-                     ((unsigned long long)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15) << 32) |
-                     ((unsigned long long)blockIdx.x << 40);   // + XCC_ID, workgroup id
+    if (lane < 24) dst[32 + 24 * wave + lane] = secacc_;
+    if (lane == 0)   // SIMD, CU, SE; XCC_ID; workgroup id
+      dst[16 + wave] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                       ((unsigned long long)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15) << 32) |
+                       ((unsigned long long)blockIdx.x << 40);
   }
   Ug = nullptr;
 #endif

@@ -14,8 +14,8 @@ import phase_stamps  # noqa: E402
 
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
-    U = phase_stamps.run_raw(B, 10, ("trot10",), 1000)
-    hw = U.reshape(B, -1).view(np.uint64)[:, 24:26].astype(np.int64)
+    slots = phase_stamps.run_raw(B, 10, ("trot10",), 1000)
+    hw = slots[:, 16:18]
     simd = (hw >> 4) & 3
     cu = (hw >> 8) & 15
     sh = (hw >> 12) & 1

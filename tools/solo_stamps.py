@@ -33,8 +33,8 @@ def one(lib, B, out):
     """One stamps build in this process (the library is loaded once per process)."""
     os.environ["MPCQP_STAMPS_LIB"] = lib
     import phase_stamps
-    U, it = phase_stamps.run_raw(B, 10, ("trot10",), 1000, with_iters=True)
-    ts = U.reshape(B, -1).view(np.uint64)[:, :7].astype(np.int64)
+    slots, it = phase_stamps.run_raw(B, 10, ("trot10",), 1000, with_iters=True)
+    ts = slots[:, :7]
     np.savez(out, cyc=ts[:, 6] - ts[:, 0], it=it)
 
 
