@@ -47,6 +47,8 @@ def parse():
                          "(LinearMpc.set_warm_start); an extra line, never the headline")
     ap.add_argument("--standing-every", type=int, default=0,
                     help="diagnostics: make every k-th robot stand (the interior-point class)")
+    ap.add_argument("--cross-leg-r", action="store_true",
+                    help="weights: the reference Q and an R coupling every pair of legs (mpcqp_set_weights)")
     ap.add_argument("--gait", default="trot10",
                     help="config1: the drop-in's gait (trot10 = Gait.TROTTING10; standing = Gait.STANDING, "
                          "the interior-point class at horizon 16)")
@@ -458,6 +460,14 @@ def main():
     # (mpcqp_set_stance_range; an all-standing fleet goes straight to the interior-point class)
     eng.set_stance_range(min_stance, max_stance)
     eng.set_order(args.order)
+    if args.cross_leg_r:   # the reference's diagonals scaled by a dense correlation matrix on R
+        from mpcqp.params import Q_DIAG, R_DIAG
+        A = np.random.default_rng(12).standard_normal((12, 12))
+        Cr = A @ A.T / 12.0 + 0.5 * np.eye(12)
+        dr = np.sqrt(np.diag(Cr))
+        sq = np.sqrt(np.asarray(R_DIAG, np.float64))
+        Rx = np.outer(sq, sq) * Cr / np.outer(dr, dr)
+        eng.set_weights(np.diag(Q_DIAG), 0.5 * (Rx + Rx.T))
     if args.warm_fleet:
         eng.set_warm_start(Bpg)
     dev_b = []
@@ -696,6 +706,8 @@ def main():
             line["gather_ms_avg"] = gather_ms
         if args.standing_every:
             line["config"]["workload"] += f", every {args.standing_every}th robot standing"
+        if args.cross_leg_r:
+            line["config"]["workload"] += ", R coupling every pair of legs (the interior-point class's 12 x 12 stage weights)"
         if args.warm_fleet:
             line["config"]["workload"] += (", warm fleet: consecutive ticks of one fleet (x0 drifting "
                                            "N(0, 2e-3) per tick), each robot's active set remembered")

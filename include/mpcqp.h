@@ -83,8 +83,9 @@ extern "C" {
 #define MPCQP_STATUS_INFEASIBLE 2  /* cannot happen for this QP (U = 0 is feasible) */
 #define MPCQP_STATUS_TOO_LARGE 3   /* stance variables exceed the engine's capacity */
 #define MPCQP_STATUS_NONFINITE 4   /* non-finite input or result */
-#define MPCQP_STATUS_UNSUPPORTED 5 /* weights the robot's capacity class cannot apply (see
-                                      mpcqp_set_weights); u0 / U are 0 */
+#define MPCQP_STATUS_UNSUPPORTED 5 /* weights the robot's capacity class cannot apply; no
+                                      weights reach it since ABI 6's cross-leg stage weights
+                                      (kept as a guard); u0 / U are 0 */
 
 typedef struct mpcqp_params {
   int32_t horizon;       /* N (LinearMpcConfig.horizon, linear_mpc_configs.py:11) */
@@ -119,9 +120,9 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
  * may still read it); only every 64th change synchronises the whole device
  * (hipDeviceSynchronize) to release the kept buffers -- not while a stream of this
  * device is being captured into a graph.
- * The interior-point class (robots with more than 128 stance variables) supports a full
- * Q and an R without cross-leg couplings (R[i][j] = 0 for legs i / 3 != j / 3); a robot of
- * that class under weights it does not support reports MPCQP_STATUS_UNSUPPORTED. */
+ * Every capacity class takes any symmetric Q and R; an R coupling different legs
+ * (R[i][j] != 0 for i / 3 != j / 3) runs the interior-point class (robots with more than 128
+ * stance variables) with whole 12 x 12 stage weights instead of per-leg blocks. */
 int mpcqp_set_weights(mpcqp_ctx* ctx, const double* Q, const double* R);
 
 /* Largest number of stance foot-steps the caller promises per robot
@@ -144,6 +145,11 @@ int mpcqp_set_stance_range(mpcqp_ctx* ctx, int32_t min_stance, int32_t max_stanc
  * horizontal velocity error |v0 - vref_0|, which tracks its active-set size -- so the longest
  * robots start first and the launch ends near its mean load.  Costs one small sort launch per
  * such solve; the results are bitwise those of mode 0 (batch order: robot b on workgroup b).
+ * The order needs the stream's queue set even for a batch class 64 solves alone: the first
+ * such call on a stream allocates it (hipMalloc + an asynchronous clear), and a later, larger
+ * batch reallocates it after a synchronisation of that stream.  To capture solves into a HIP
+ * graph, make one call of at least the captured batch size on the capture stream first, or
+ * set mode 0 (a class-64-only solve in batch order allocates nothing).
  * MPCQP_ERR_ARG for any other mode. */
 int mpcqp_set_order(mpcqp_ctx* ctx, int32_t mode);
 

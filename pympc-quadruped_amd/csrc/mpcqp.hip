@@ -572,7 +572,8 @@ __device__ __forceinline__ int ipm_claim_slot(unsigned* bits, int nw, int start)
 // a global slot claimed for the robot's solve (sbits: slot bitmap, nsw words)
 // One wave per SIMD at most (LDS bounds a CU to 3 or 4 of these workgroups): the wave may take
 // the whole 512-register file, so values beyond the 256 arch VGPRs live in AGPRs, not scratch
-template <bool FULL, int NM, bool MG = false>
+// XR: an R with cross-leg couplings (full-weight latency layouts only)
+template <bool FULL, int NM, bool MG = false, bool XR = false>
 __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(1, 1))) void mpcqp_kernel_ipm(
     KParams P, const float* __restrict__ x0g, const float* __restrict__ xrefg,
     const float* __restrict__ contactg, const float* __restrict__ feetg, const float* __restrict__ robotg,
@@ -590,7 +591,7 @@ __global__ __launch_bounds__(LANES) __attribute__((amdgpu_waves_per_eu(1, 1))) v
   int slot = 0;
   if (tid == 0) slot = ipm_claim_slot(sbits, nsw, k % nsw);
   slot = __builtin_amdgcn_readlane(slot, 0);
-  solve_robot_ipm<FULL, NM, MG>(P, b, sm, sscratch + (size_t)slot * IpmSlot<NM>::SIZE, x0g, xrefg, contactg, feetg, robotg, u0g,
+  solve_robot_ipm<FULL, NM, MG, XR>(P, b, sm, sscratch + (size_t)slot * IpmSlot<NM>::SIZE, x0g, xrefg, contactg, feetg, robotg, u0g,
                             Ug, statusg, itersg);
   if (tid == 0) {
     atomicAnd(&sbits[slot >> 5], ~(1u << (slot & 31)));   // the solve's S_k reads are done
@@ -650,6 +651,7 @@ struct mpcqp_ctx {
   double* sscratch;
   int sslots;
   double* wdev;       // full Q (13 x 13) then R (12 x 12) on the device (mpcqp_set_weights); nullptr: diagonal
+  bool xr;            // R couples different legs: the interior-point class's XR instantiations
   double q_full[13 * 13];   // the current weights as whole matrices (host copies: a NULL argument
   double r_full[12 * 12];   // of mpcqp_set_weights keeps that matrix, off-diagonal entries included)
   std::vector<double*> retired;   // earlier full-weight buffers (in-flight solves may read them)
@@ -801,6 +803,7 @@ int mpcqp_create(const mpcqp_params* p, int32_t device, mpcqp_ctx** out) {
   ctx->sscratch = nullptr;
   ctx->sslots = 0;
   ctx->wdev = nullptr;
+  ctx->xr = false;
   ctx->warm = nullptr;
   ctx->warm_cap = 0;
   for (int i = 0; i < 13 * 13; ++i) ctx->q_full[i] = (i % 14 == 0) ? p->q_diag[i / 14] : 0.0;
@@ -914,9 +917,10 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
       ctx->sscratch = nullptr;
       return set_err(ctx, MPCQP_ERR_ALLOC, "interior-point scratch allocation failed");
     }
-    // the slot bitmap after the slots: all free (every solve releases its slot); synchronous,
-    // so a launch on any stream of the context finds it cleared
-    if (hipMemset((char*)ctx->sscratch + sbytes, 0, slots / 8) != hipSuccess) {
+    // the slot bitmap after the slots: all free (every solve releases its slot); cleared on this
+    // stream and waited for, so a launch on any stream of the context finds it cleared
+    if (hipMemsetAsync((char*)ctx->sscratch + sbytes, 0, slots / 8, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
       (void)hipFree(ctx->sscratch);
       ctx->sscratch = nullptr;
       return set_err(ctx, MPCQP_ERR_HIP, "interior-point scratch init failed");
@@ -935,9 +939,13 @@ int mpcqp_solve(mpcqp_ctx* ctx, int32_t batch, const float* x0, const float* xre
     // class takes a batch larger than three robots per CU can hold at once; otherwise -- a
     // single drop-in robot, or robots queued from a mixed batch, whose latency is the
     // launch's tail -- the latency layout (M_k in LDS, three per CU)
+    // A cross-leg R (ctx->xr) takes the XR instantiations: 12 x 12 stage weights, latency layouts.
     const bool thru = first == 3 && batch > 3 * ctx->ncu;
-    auto kern = kp.N <= 16 ? (thru ? (full ? mpcqp_kernel_ipm<true, 16, true> : mpcqp_kernel_ipm<false, 16, true>)
-                                   : (full ? mpcqp_kernel_ipm<true, 16> : mpcqp_kernel_ipm<false, 16>))
+    auto kern = ctx->xr ? (kp.N <= 16 ? mpcqp_kernel_ipm<true, 16, false, true>
+                           : kp.N <= kDenseN ? mpcqp_kernel_ipm<true, kDenseN, false, true>
+                                             : mpcqp_kernel_ipm<true, kMaxN, false, true>)
+                : kp.N <= 16 ? (thru ? (full ? mpcqp_kernel_ipm<true, 16, true> : mpcqp_kernel_ipm<false, 16, true>)
+                                     : (full ? mpcqp_kernel_ipm<true, 16> : mpcqp_kernel_ipm<false, 16>))
                 : kp.N <= kDenseN ? (full ? mpcqp_kernel_ipm<true, kDenseN> : mpcqp_kernel_ipm<false, kDenseN>)
                                   : (full ? mpcqp_kernel_ipm<true, kMaxN> : mpcqp_kernel_ipm<false, kMaxN>);
     // one workgroup per robot of the batch (the queued ones beyond the count exit at once)
@@ -1029,7 +1037,7 @@ int mpcqp_set_weights(mpcqp_ctx* ctx, const double* Q, const double* R) {
     rmax = fmax(rmax, fabs(r[i]));
   }
   if (!finite) return set_err(ctx, MPCQP_ERR_ARG, "weights: non-finite entry");
-  bool diag = true;
+  bool diag = true, cross = false;
   for (int i = 0; i < NX; ++i)
     for (int j = 0; j < NX; ++j) {
       if (fabs(q[i * NX + j] - q[j * NX + i]) > 1e-12 * qmax) return set_err(ctx, MPCQP_ERR_ARG, "weights: Q not symmetric");
@@ -1039,6 +1047,7 @@ int mpcqp_set_weights(mpcqp_ctx* ctx, const double* Q, const double* R) {
     for (int j = 0; j < NU; ++j) {
       if (fabs(r[i * NU + j] - r[j * NU + i]) > 1e-12 * rmax) return set_err(ctx, MPCQP_ERR_ARG, "weights: R not symmetric");
       if (i != j && r[i * NU + j] != 0.0) diag = false;
+      if (i / 3 != j / 3 && r[i * NU + j] != 0.0) cross = true;
     }
   DeviceScope dev(ctx->device);
   if (!dev.ok) return set_err(ctx, MPCQP_ERR_HIP, "hipSetDevice failed");
@@ -1071,6 +1080,7 @@ int mpcqp_set_weights(mpcqp_ctx* ctx, const double* Q, const double* R) {
     ctx->retired.push_back(ctx->wdev);
   }
   ctx->wdev = nb;   // nullptr: the diagonal fast path (the weights live in the kernel arguments)
+  ctx->xr = cross;
   memcpy(ctx->q_full, q, sizeof(q));
   memcpy(ctx->r_full, r, sizeof(r));
   for (int i = 0; i < NX; ++i) ctx->params.q_diag[i] = q[i * (NX + 1)];

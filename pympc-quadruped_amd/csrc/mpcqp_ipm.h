@@ -137,12 +137,14 @@ static_assert(sizeof(IpmSharedT<16, false, true>) <= 160 * 1024 / 4, "N <= 16, d
 static_assert(sizeof(IpmSharedT<16, true, true>) <= 160 * 1024 / 3, "N <= 16, full weights: three robots per CU");
 static_assert(sizeof(IpmSharedT<16, true, false>) <= 160 * 1024 / 3, "N <= 16, M_k in LDS: three robots per CU");
 // One robot's global slot (doubles): S_k, then -- used by the four-per-CU layout at NM = 16
-// only -- M_k, M_k^T and the saved iterate.  The stride depends on the stage count alone, so
-// one pool per context (sized for its horizon) serves both N <= 16 layouts.
+// only -- M_k, M_k^T and the saved iterate.  A cross-leg R (XR) keeps its 12 x 12 stage weights
+// W_k at offset W: the latency layouts it runs in hold M_k in LDS, so at NM = 16 they take M's
+// place.  The stride depends on the stage count alone, so one pool per context (sized for its
+// horizon) serves every layout.
 template <int NM>
 struct IpmSlot {
-  static constexpr int M = NM * 144, MT = 2 * NM * 144, US = 3 * NM * 144;
-  static constexpr int SIZE = NM <= 16 ? 3 * NM * 144 + NM * NU : NM * 144;
+  static constexpr int M = NM * 144, MT = 2 * NM * 144, US = 3 * NM * 144, W = NM * 144;
+  static constexpr int SIZE = NM <= 16 ? 3 * NM * 144 + NM * NU : 2 * NM * 144;
 };
 // the slot stride of the layouts a context of horizon N launches (host and device)
 __host__ __device__ constexpr int ipm_slot_doubles(int N) {
@@ -202,7 +204,10 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 }
 
 // One robot with more than 128 stance variables.  Called by a 64-thread workgroup.
-template <bool FULL, int NM, bool MG>
+// XR: the weights' R couples different legs (mpcqp_set_weights; FULL and the latency layout):
+// the stage weights W_k are then whole 12 x 12 matrices (stage_weights below) instead of the
+// foot-steps' 3 x 3 blocks.
+template <bool FULL, int NM, bool MG, bool XR = false>
 __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSharedT<NM, FULL, MG>& sm, double* __restrict__ Sg,
                                                 const float* __restrict__ x0g, const float* __restrict__ xrefg,
                                                 const float* __restrict__ contactg, const float* __restrict__ feetg,
@@ -227,7 +232,8 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     write_empty_t<NT>(b, lane, N, MPCQP_STATUS_OK, u0g, Ug, statusg, itersg);
     return;
   }
-  if constexpr (FULL) {   // full weights: cross-leg R couplings break the per-foot-step weights
+  static_assert(!XR || (FULL && !MG), "a cross-leg R runs in the full-weight latency layouts");
+  if constexpr (FULL && !XR) {   // the host routes a cross-leg R to the XR instantiation: a guard
     bool cross = false;
     for (int e = lane; e < NU * NU; e += NT)
       cross |= (e / NU) / 3 != (e % NU) / 3 && KP.wfull[NX * NX + e] != 0.0;
@@ -481,8 +487,13 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     for (int e = lane; e < N * NU; e += NT) {   // stage gradients R u_k + B_d^T nu_k
       const int k = e / NU, c = e % NU;
       double ru;
-      if constexpr (FULL) {
-        const int c3 = 3 * (c / 3);   // Rh's leg block (no cross-leg couplings in this class)
+      if constexpr (XR) {   // the whole row of Rh (swing entries of U are 0)
+        double r12[12], u12[12];
+        ld12(r12, sm.wf.rf[c]);
+        ld12(u12, sm.U[k]);
+        ru = dot12(r12, u12);
+      } else if constexpr (FULL) {
+        const int c3 = 3 * (c / 3);   // Rh's leg block (no cross-leg couplings in this instantiation)
         ru = fma(sm.wf.rf[c][c3 + 2], sm.U[k][c3 + 2], fma(sm.wf.rf[c][c3 + 1], sm.U[k][c3 + 1], sm.wf.rf[c][c3] * sm.U[k][c3]));
       } else {
         ru = sm.rh[c] * sm.U[k][c];
@@ -511,6 +522,22 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
   // previous one are issued before the sweep, so the matrix cores run them under it.
   auto stage_e = [&](int k) -> d4 {   // E_k
     d4 Er = diag4(0.0);
+    if constexpr (XR) {   // (W_k B_d^T)[c][lc] = W_k row c . B_d row lc (W_k: 0 on swing rows)
+      double brow[12];
+      ld12(brow, sm.Bm[lcc]);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int c = 4 * q + lr;
+        double x = 0.0;
+        if (c < 12 && lc < 12) {
+          double wr[12];
+          ld12g(wr, Sg + IpmSlot<NM>::W + k * 144 + 12 * c);
+          x = dot12(wr, brow);
+        }
+        Er = mfma(Bop[q], x, Er);
+      }
+      return Er;
+    }
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       const int c = 4 * q + lr;
@@ -636,6 +663,18 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
   // W_k (z_k - sub_k) restricted to entry c (leg l = c / 3), z_k = B_d^T x_k precomputed for every
   // stage by stage_gemm; 0 for a swing leg
   auto wz = [&](int k, int c, const double (*z)[NU], const double* sub) -> double {
+    if constexpr (XR) {   // W_k row c . (z_k - sub)
+      double wr[12], zv[12];
+      ld12g(wr, Sg + IpmSlot<NM>::W + k * 144 + 12 * c);
+      ld12(zv, z[k]);
+      if (sub) {
+        double sv[12];
+        ld12(sv, sub);
+#pragma unroll
+        for (int i = 0; i < 12; ++i) zv[i] -= sv[i];
+      }
+      return dot12(wr, zv);
+    }
     const int l = c / 3, a = c % 3;
     const int j = sm.mt.stance_of[4 * k + l];
     if (j < 0) return 0.0;
@@ -665,7 +704,9 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       const int k = e / NU, c = e % NU, l = c / 3, a = c % 3;
       const int j = sm.mt.stance_of[4 * k + l];
       double v = 0.0;
-      if (j >= 0) {
+      if constexpr (XR) {
+        v = wz(k, c, sm.rhs, nullptr);
+      } else if (j >= 0) {
         const double* wj = sm.W[j] + 3 * a;
         v = wj[0] * sm.rhs[k][3 * l] + wj[1] * sm.rhs[k][3 * l + 1] + wj[2] * sm.rhs[k][3 * l + 2];
       }
@@ -787,6 +828,86 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     IPM_T1(2);
   };
 
+  // XR: the stage weights W_k (IpmSlot::W, 12 x 12 row-major) over the stage's stance entries
+  // (swing rows / columns 0), from the foot-steps' blocks in sm.W[j]: the interior point's
+  // G_j^T D_j G_j, W_k = (Rh + blockdiag G_j^T D_j G_j)^-1, or the polish's null-space projectors
+  // P_j, W_k = P (P Rh P + I - P)^-1 P with P = blockdiag P_j -- the per-foot-step weights of the
+  // leg-block instantiations with Rh's cross-leg blocks kept.  One stage at a time, Gauss-Jordan
+  // on [A | I] or [A | P] (A SPD, no pivoting): lane c < 12 holds column c of A, lane 12 + c
+  // column c of the right-hand side; the pivot column by readlane, as in factor().
+  auto stage_weights = [&](bool pol) {
+    if constexpr (XR) {
+      const int jc = lane < 12 ? lane : (lane < 24 ? lane - 12 : 0);
+      const int lj = jc / 3, cj = jc % 3;
+      const bool rhs = lane >= 12;
+      for (int k = 0; k < N; ++k) {
+        const int fc = lane < 24 ? sm.mt.stance_of[4 * k + lj] : -1;   // this lane's column foot-step
+        int fl[4];   // each leg's foot-step at stage k (-1: swing), wave-uniform
+#pragma unroll
+        for (int l = 0; l < 4; ++l) fl[l] = uni(sm.mt.stance_of[4 * k + l]);
+        double pcol[3] = {0.0, 0.0, 0.0};   // column cj of P_fc (polish)
+        if (pol && fc >= 0) {
+#pragma unroll
+          for (int a = 0; a < 3; ++a) pcol[a] = sm.W[fc][3 * a + cj];
+        }
+        double t[12];   // polish: (Rh P)[m][jc]
+#pragma unroll
+        for (int m = 0; m < 12; ++m) {
+          const double* r = &sm.wf.rf[m][3 * lj];
+          t[m] = pol ? fma(r[2], pcol[2], fma(r[1], pcol[1], r[0] * pcol[0])) : 0.0;
+        }
+        double col[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+          const int li = i / 3, ai = i % 3;
+          const int fi = fl[li];
+          double v;
+          if (rhs) {   // e_jc, or column jc of P
+            v = pol ? (li == lj ? pcol[ai] : 0.0) : (i == jc ? 1.0 : 0.0);
+          } else if (fi < 0 || fc < 0) {   // a swing leg's rows / columns: the identity
+            v = i == jc ? 1.0 : 0.0;
+          } else if (!pol) {   // Rh + G^T D G on the leg's block
+            v = sm.wf.rf[i][jc] + (li == lj ? sm.W[fc][3 * ai + cj] : 0.0);
+          } else {   // P Rh P + I - P
+            const double* pi = sm.W[fi] + 3 * ai;   // row ai of P_fi
+            v = fma(pi[2], t[3 * li + 2], fma(pi[1], t[3 * li + 1], pi[0] * t[3 * li]));
+            if (li == lj) v += (i == jc ? 1.0 : 0.0) - pcol[ai];
+          }
+          col[i] = v;
+        }
+#pragma unroll
+        for (int kk = 0; kk < 12; ++kk) {
+          double pc[12];
+#pragma unroll
+          for (int i = 0; i < 12; ++i) pc[i] = readlane_d(col[i], kk);
+          const double ip = rcp_nr(pc[kk]);
+          const double rowv = col[kk] * ip;
+#pragma unroll
+          for (int i = 0; i < 12; ++i) col[i] = (i == kk) ? rowv : fma(-pc[i], rowv, col[i]);
+        }
+        if (rhs && lane < 24) {   // column jc of W_k: A^-1 (stance block), or P A^-1 P
+#pragma unroll
+          for (int i = 0; i < 12; ++i) {
+            const int li = i / 3, ai = i % 3;
+            const int fi = fl[li];
+            double w = 0.0;
+            if (fi >= 0 && fc >= 0) {
+              if (pol) {
+                const double* pi = sm.W[fi] + 3 * ai;
+                w = fma(pi[2], col[3 * li + 2], fma(pi[1], col[3 * li + 1], pi[0] * col[3 * li]));
+              } else {
+                w = col[i];
+              }
+            }
+            Sg[IpmSlot<NM>::W + k * 144 + 12 * i + jc] = w;
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // the W_k stores, before stage_e / wz read them
+      fsync<NT>();
+    }
+  };
+
   int status = MPCQP_STATUS_MAX_ITER;
   int nfact = 0;
 #ifdef MPCQP_IPM_DEBUG
@@ -820,7 +941,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       ipm_foot_nullspace(rw, FACT(j) & liv, -sm.mt.ub[j], rh, pj, fp, wv);
 #pragma unroll
       for (int e = 0; e < 9; ++e) {
-        sm.W[j][e] = wv[e];
+        sm.W[j][e] = XR ? pj[e] : wv[e];   // XR: the projector, for stage_weights
         FPJ(j)[e] = pj[e];
       }
       double* u = foot_ptr(j, sm.U);
@@ -829,6 +950,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       u[2] = fp[2];
     }
     fsync<NT>();
+    stage_weights(true);
     factor();
     ++nfact;
     for (int rf = 0; rf < IPM_NREF; ++rf) {
@@ -940,12 +1062,14 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
 #pragma unroll
       for (int r = 0; r < 6; ++r) d[r] = 1e-2;
       legrh(j, rh);
-      ipm_foot_weight(rw, liv, d, rh, wv);
+      if constexpr (XR) ipm_foot_gdg(rw, liv, d, wv);   // the leg's block of the stage weight
+      else ipm_foot_weight(rw, liv, d, rh, wv);
 #pragma unroll
       for (int e = 0; e < 9; ++e) sm.W[j][e] = wv[e];
     }
     for (int e = lane; e < N * NU; e += NT) sm.rhs[e / NU][e % NU] = -sm.gr[e / NU][e % NU];
     fsync<NT>();
+    stage_weights(false);
     factor();
     ++nfact;
     lsolve();
@@ -1032,11 +1156,13 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
 #pragma unroll
       for (int r = 0; r < 6; ++r) d[r] = ((liv >> r) & 1) ? FL(j)[r] / FS(j)[r] : 0.0;
       legrh(j, rh);
-      ipm_foot_weight(rw, liv, d, rh, wv);
+      if constexpr (XR) ipm_foot_gdg(rw, liv, d, wv);
+      else ipm_foot_weight(rw, liv, d, rh, wv);
 #pragma unroll
       for (int e = 0; e < 9; ++e) sm.W[j][e] = wv[e];
     }
     fsync<NT>();
+    stage_weights(false);
     factor();
     ++nfact;
     // Newton direction for the complementarity target: predictor (sig = 0, corr = false)

@@ -238,3 +238,15 @@ __host__ __device__ inline void ipm_foot_weight(const double (&rw)[6][3], int li
     }
   inv3(a, W);
 }
+
+// G^T D G of a foot-step: sum_r d_r a_r a_r^T over the rows in `live` (bit r) -- the block a
+// cross-leg R's stage weight adds on the foot's leg before the stage inversion (mpcqp_ipm.h).
+__host__ __device__ inline void ipm_foot_gdg(const double (&rw)[6][3], int live, const double (&d)[6], double (&o)[9]) {
+  for (int x = 0; x < 3; ++x)
+    for (int y = 0; y < 3; ++y) {
+      double v = 0.0;
+      for (int r = 0; r < 6; ++r)
+        if ((live >> r) & 1) v += d[r] * rw[r][x] * rw[r][y];
+      o[3 * x + y] = v;
+    }
+}

@@ -62,12 +62,6 @@ def _weight_matrix(W, n, name):
     return W.copy()
 
 
-def _cross_leg(R):
-    """True when R has a nonzero entry between two different legs' 3x3 blocks."""
-    leg = np.arange(12) // 3
-    return bool(np.any(R[leg[:, None] != leg[None, :]] != 0.0))
-
-
 class ModelPredictiveController():
 
     def __init__(self, mpc_config, robot_config):
@@ -96,17 +90,6 @@ class ModelPredictiveController():
         self.com_height_des = robot_config.base_height_des
         self.Q = _weight_matrix(mpc_config.Q, 13, "Q")
         self.R = _weight_matrix(mpc_config.R, 12, "R")
-        if _cross_leg(self.R) and int(self.horizon) > 20:
-            # N > 20: every schedule goes to the interior-point class, which takes leg-block
-            # R only -- no tick could be solved
-            raise ValueError(f"LinearMpcConfig.R couples different legs; at horizon {self.horizon} every "
-                             "schedule runs in the engine's interior-point class, which supports leg-block R only")
-        if _cross_leg(self.R) and 12 * int(self.horizon) > 128:
-            # 128 < 12 N: trot / pace / bound schedules stay in the dense classes (any symmetric
-            # R); only schedules with more than 128 stance variables (standing) reach the
-            # interior-point class, whose ticks then raise (status UNSUPPORTED)
-            warnings.warn(f"LinearMpcConfig.R couples different legs: at horizon {self.horizon} schedules with "
-                          "more than 128 stance variables (e.g. Gait.STANDING) cannot be solved and raise")
         I = np.asarray(self.base_inertia_base, dtype=np.float32)
         self._robot_record = pack_robot(
             dict(mass=float(self.mass), fz_max=float(self.fz_max), mu=float(self.mu),

@@ -96,8 +96,8 @@ class LinearMpc:
 
     def set_weights(self, Q, R):
         """Replace the cost weights (include/mpcqp.h mpcqp_set_weights): diagonals or full
-        symmetric matrices.  A cross-leg R entry is not supported by the interior-point
-        class (n > 128 variables): those robots return MPCQP_STATUS_UNSUPPORTED."""
+        symmetric matrices (every capacity class takes any symmetric Q and R; a cross-leg R
+        runs the interior-point class's 12 x 12 stage-weight instantiations)."""
         qd, qf = _weights(Q, 13, "Q")
         rd, rf = _weights(R, 12, "R")
         qm = np.ascontiguousarray(qf if qf is not None else np.diag(qd), dtype=np.float64)

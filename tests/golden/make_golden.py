@@ -20,7 +20,9 @@ SURVEY.md Appendix A), then:
                         (kinematics.py:40-71) on float32 quaternions, and
                         LegController.update's stance branch (leg_controller.py:86-89)
 
-  formulation_full_N{N}.npz  the same for full (non-diagonal) Q and R (--full N)
+  formulation_full_N{N}.npz  the same for full (non-diagonal) Q and R (--full N): leg-block R
+                        at N = 10 / 16, an R coupling every pair of legs at N = 20 / 24 (the
+                        interior-point class's 12 x 12 stage weights), standing robots included
 
 Usage:  python tests/golden/make_golden.py            (all horizons, subprocesses)
         python tests/golden/make_golden.py --horizon 10
@@ -143,10 +145,12 @@ def gen(horizon):
     print(f"N={N}: max KKT {np.array(kkts).max():.2e}, iterations {iters}, rounding-level stops {rounding}")
 
 
-def full_weights(seed):
+def full_weights(seed, cross_leg=False):
     """A symmetric positive-semidefinite Q coupling the moving state components (the
     reference's diagonal scaled by a correlation matrix, |rho| <= 0.4; state 12 keeps
-    weight 0) and an R with full 3 x 3 leg blocks (mpc.py:49-52 take whole matrices)."""
+    weight 0) and an R with full 3 x 3 leg blocks (mpc.py:49-52 take whole matrices) --
+    or, cross_leg, an R coupling every pair of legs (the diagonal scaled by a dense random
+    correlation matrix)."""
     rng = np.random.default_rng(seed)
     C = np.eye(13)
     for _ in range(12):
@@ -162,6 +166,11 @@ def full_weights(seed):
     for leg in range(4):
         S = rng.uniform(-0.3, 0.3, size=(3, 3))
         R[3 * leg:3 * leg + 3, 3 * leg:3 * leg + 3] += 1e-5 * (S @ S.T)
+    if cross_leg:
+        A = rng.standard_normal((12, 12))
+        Cr = A @ A.T / 12.0 + 0.5 * np.eye(12)
+        dr = np.sqrt(np.diag(Cr))
+        R = 1e-5 * Cr / np.outer(dr, dr)
     return 0.5 * (Q + Q.T), 0.5 * (R + R.T)
 
 
@@ -175,7 +184,7 @@ def gen_full(horizon):
     from mpcqp.synthetic import make_batch
     from mpcqp.params import robot_from_config
     N = horizon
-    Qf, Rf = full_weights(500 + N)
+    Qf, Rf = full_weights(500 + N, cross_leg=N >= 20)
 
     class FullWeights(LinearMpcConfig):
         Q = Qf
@@ -199,7 +208,9 @@ def gen_full(horizon):
         Ad, Bd = c._discretize_continuous_model(Ac, Bc)
         H, g = c._generate_QP_cost(Ad, Bd, c.current_state, bt["xref"][b].reshape(-1))
         C, lb, ub = c._generate_QP_constraints(bt["contact"][b].reshape(-1))
-        x, _, _ = Q.solve_qp_dual_active_set(H, g, C, lb, ub)
+        x, y, info = Q.solve_qp_dual_active_set(H, g, C, lb, ub)
+        k = Q.kkt_residuals(H, g, C, lb, ub, x, y)
+        assert max(k["stationarity"], k["primal"], k["dual"], k["complementarity"]) < 1e-7, (N, b, k)
         Hp.append([H @ v for v in probe])
         gs.append(g)
         us.append(x)
@@ -207,7 +218,7 @@ def gen_full(horizon):
                         contact=bt["contact"], feet=bt["feet"], robot=bt["robot"], robot_name=np.array(names),
                         Q=Qf, R=Rf, H_probe=np.array(Hp), probe=probe, g=np.array(gs), u_star=np.array(us),
                         horizon=N, dt=0.05)
-    print(f"full weights N={N}: {B} cases")
+    print(f"full weights N={N}: {B} cases, stance counts {[int(v) for v in (bt['contact'] > 0).reshape(B, -1).sum(1)]}")
 
 
 class _FakeRobotData:
