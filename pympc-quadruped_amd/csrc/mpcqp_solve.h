@@ -824,6 +824,14 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     // method's convergence argument is unchanged; otherwise p takes the usual step.
     if (p2 >= 0) {
       CNT(3);
+      // the slot directions r, r2 first: their loads overlap the 2 x 2 solve below, which no
+      // longer branches (tp, tq, id are used only when ok, as before)
+      double rs1[VPL], rs2[VPL];
+#pragma unroll
+      for (int k = 0; k < VPL; ++k) {
+        rs1[k] = vr[lane + LANES * k];
+        rs2[k] = vr2[lane + LANES * k];
+      }
       double zs2[CPL];
 #pragma unroll
       for (int k = 0; k < CPL; ++k) zs2[k] = cdot(vz2, k);
@@ -836,20 +844,13 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       const double s12 = sgpr_d(readlane_d(v12, p & 63));    // a_p . z2
       const double s22 = sgpr_d(readlane_d(v22, p2 & 63));   // a_p2 . z2
       const double det = zsp * s22 - s12 * s12;
-      bool ok = zsp > thr && s22 > thr2 && det > thr2 * zsp;
-      double tp = 0.0, tq = 0.0, id = 0.0;
-      if (ok) {
-        id = rcp_nr(det);
-        tp = sgpr_d((s12 * sp2 - s22 * sp) * id);
-        tq = sgpr_d((s12 * sp - zsp * sp2) * id);
-        ok = tp > 0.0 && tq > 0.0;
-      }
-      double rs1[VPL], rs2[VPL];
+      const double id = rcp_nr(det);
+      const double tp = sgpr_d((s12 * sp2 - s22 * sp) * id);
+      const double tq = sgpr_d((s12 * sp - zsp * sp2) * id);
+      const bool ok = zsp > thr && s22 > thr2 && det > thr2 * zsp && tp > 0.0 && tq > 0.0;
       int bad = 0;
 #pragma unroll
       for (int k = 0; k < VPL; ++k) {
-        rs1[k] = vr[lane + LANES * k];
-        rs2[k] = vr2[lane + LANES * k];
         const bool mine = (occ[k] >> lane) & 1ull;
         bad |= mine && fma(-tq, rs2[k], fma(-tp, rs1[k], u[k])) < 0.0;
       }
@@ -966,6 +967,15 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       }
     }
     SEC(11);
+    // 1 / (a_p . z) and the primal step t2 = -s_p / (a_p . z), issued ahead of the ratio test,
+    // which does not feed them: their division chain overlaps its loads and divisions, and the
+    // add reuses the reciprocal (the operations of rcp_nr(zsp) and div_nr(-sp, zsp))
+    const double is = rcp_nr(zsp);
+    double t2 = INFINITY;
+    if (zsp > thr) {
+      const double q = -sp * is;
+      t2 = fma(fma(-zsp, q, -sp), is, q);
+    }
     double rs[VPL], zx[VPL];
     double rbest = INFINITY;
     int lk = 0;
@@ -983,8 +993,6 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
     const int ll = wave_argmin_d(rbest, t1);
     const int l = ll + LANES * uni(__builtin_amdgcn_readlane(lk, ll));
     SEC(12);
-    double t2 = INFINITY;
-    if (zsp > thr) t2 = div_nr(-sp, zsp);
     const bool add = t2 <= t1;
     const double tstep = add ? t2 : t1;
     if (!(tstep < INFINITY)) {
@@ -1012,7 +1020,6 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
 #pragma unroll
       for (int k = VPL - 1; k >= 0; --k)
         if (~occ[k]) q = LANES * k + __builtin_ctzll(~occ[k]);
-      const double is = rcp_nr(zsp);
       double zr4[4], rr4[4];
       constexpr bool kSlotCoef1 = NV == 64;
       if constexpr (kSlotCoef1) {   // R's row coefficient once per slot lane (as the pair step's)
