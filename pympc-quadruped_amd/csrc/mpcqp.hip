@@ -259,6 +259,10 @@ __device__ __forceinline__ void ld4s(double (&v)[4], const double* p) {
   const d2 a = reinterpret_cast<const d2*>(p)[0], b = reinterpret_cast<const d2*>(p)[1];
   v[0] = a[0]; v[1] = a[1]; v[2] = b[0]; v[3] = b[1];
 }
+__device__ __forceinline__ void st4s(double* p, const double (&v)[4]) {
+  reinterpret_cast<d2*>(p)[0] = d2{v[0], v[1]};
+  reinterpret_cast<d2*>(p)[1] = d2{v[2], v[3]};
+}
 __device__ __forceinline__ void ld4(double (&v)[4], const double* base, int k) {
   const d2* p = reinterpret_cast<const d2*>(base + 4 * k);
   const d2 a = p[0], b = p[1];

@@ -85,6 +85,9 @@ struct alignas(16) SharedT {
     alignas(16) double vr2[2][Cfg<NV>::VEC];   // in the loop: r2 = R a_p2 of a pair step
   };
   alignas(16) double rl[Cfg<NV>::VEC];      // drop path: R_l, H R_l^T, R H R_l^T
+  // class 128: z = P a_p again in the sweep's strided layout (double-buffered by iteration), for the
+  // add pass's tile-column reads (unpadded, class 128's 16 tile columns fold 4-way on the banks)
+  alignas(16) double zp[NV == 128 ? 2 * Cfg<NV>::SVEC : 2];
   alignas(16) double tv[Cfg<NV>::VEC];
   alignas(16) double yv[Cfg<NV>::VEC];
   double wmax[Cfg<NV>::NW];
@@ -547,7 +550,8 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   // the cone rows' coefficients (lanes 0..17: row r's a_i at 3 r + i) and dependency
   // thresholds 1e-12 |a_r|^2 wscale (lanes 18..23) in one register, read by v_readlane into
   // SGPRs when a row is chosen (an LDS load + readfirstlane chain otherwise)
-  constexpr bool kRowTab = NV <= 96;   // class 128: no VGPRs to spare (an 8-byte spill)
+  constexpr bool kRowTab = NV <= 96;
+  constexpr bool kZp = NV == 128;   // z's strided copy (SharedT::zp)   // class 128: no VGPRs to spare (an 8-byte spill)
   double rowtab = 0.0;
   if (!kRowTab) {
   } else if (lane < 18) rowtab = sm.mt.rows[lane / 3][lane % 3];
@@ -794,12 +798,16 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
       if (tc == tA) {
         st4(dz, tr, zq);
         st4(dr, tr, rq);
+        // class 128: z also in the sweep's strided layout (tile-column stride TS), for the add
+        // pass's conflict-free tile-column reads (cdot and the per-lane reads keep the plain one)
+        if constexpr (kZp) st4s(sm.zp + (it & 1) * C::SVEC + i4s, zq);
       }
     };
     const int buf = it & 1;
     double* const vz = sm.vz[buf];
     double* const vr = sm.vr[buf];
     double* const vz2 = sm.zc[buf];
+    double* const vzp = sm.zp + buf * C::SVEC;   // kZp: z in the strided layout
     double* const vr2 = sm.vr2[buf];
     combo_store(c0, tcA, a0, a1, a2, vz, vr);
     if (p2 >= 0) combo_store(c02, tcA2, b0, b1, b2, vz2, vr2);
@@ -1026,8 +1034,13 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
         sm.tv[lane] = ((lane == q) ? 1.0 - rs[0] : -rs[0]) * is;
         fsync<LANES>();
       }
-      ld4(zr4, vz, tr);
-      ldt<TW>(cv, vz, tc);
+      if constexpr (kZp) {
+        ld4s(zr4, vzp + i4s);
+        lds_t<TW, C::TS>(cv, vzp, tc);
+      } else {
+        ld4(zr4, vz, tr);
+        ldt<TW>(cv, vz, tc);
+      }
       ld4(rr4, kSlotCoef1 ? sm.tv : vr, tr);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
