@@ -550,8 +550,8 @@ __device__ __forceinline__ void solve_robot(const KParams& P, int b, SharedT<NV>
   // the cone rows' coefficients (lanes 0..17: row r's a_i at 3 r + i) and dependency
   // thresholds 1e-12 |a_r|^2 wscale (lanes 18..23) in one register, read by v_readlane into
   // SGPRs when a row is chosen (an LDS load + readfirstlane chain otherwise)
-  constexpr bool kRowTab = NV <= 96;
-  constexpr bool kZp = NV == 128;   // z's strided copy (SharedT::zp)   // class 128: no VGPRs to spare (an 8-byte spill)
+  constexpr bool kRowTab = NV <= 96;   // class 128: no VGPRs to spare (an 8-byte spill)
+  constexpr bool kZp = NV == 128;      // z's strided copy (SharedT::zp)
   double rowtab = 0.0;
   if (!kRowTab) {
   } else if (lane < 18) rowtab = sm.mt.rows[lane / 3][lane % 3];
