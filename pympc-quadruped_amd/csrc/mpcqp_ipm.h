@@ -123,7 +123,7 @@ struct alignas(16) IpmSharedT {
   double rh[NU];                   // 2 r
   [[no_unique_address]] std::conditional_t<FULL, IpmWFull, IpmEmpty> wf;   // full weights only
   double W[IPM_NF][9];             // per stance foot-step 3x3 weight of the Newton system
-  alignas(16) double P[144];       // P_{k+1}
+  alignas(16) double QT[144];      // T^-T Qh T^-1, the factorisation's stage cost (12 x 12)
   alignas(16) double U[NM][NU];    // iterate (swing entries 0)
   alignas(16) double dU[NM][NU];
   alignas(16) double rhs[NM][NU];
@@ -553,14 +553,72 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     }
     return Er;
   };
+  // The factorisation runs in the basis x~ = T x, T = I - Nm / 2 (12-state: Nm maps rows 6..11
+  // into rows 0..5, so Nm^2 = 0 and T^-1 = I + Nm / 2).  There B_d = T^-1 [0; B6] (B6 = B_d's
+  // rows 6..11: rows 0..5 of B_d are (h^2 / 2) R_z^T K and h^2 / 2m, i.e. Nm / 2 of rows 6..11 --
+  // the midpoint rule), T A_d T^-1 = A_d, the stage cost is Qt = T^-T Qh T^-1, and
+  // E~_k = diag(0, C_k) with C_k = E_k[6:12, 6:12] = B6 W_k B6^T.  Riccati on P~ = T^-T P T^-1:
+  //   K = P~[6:12, 6:12], V = P~[6:12, :], G = (I + C K)^-1, Y = G C = (C^-1 + K)^-1 (6 x 6),
+  //   S~ = (I + P~ E~)^-1 P~ = P~ - V^T Y V,   P~_k = Qt + A^T S~ A   (Woodbury),
+  // one Gauss-Jordan on [I + C K | C | I] -- 6 pivots over 18 lanes, 6-entry pivot columns --
+  // in place of [I + P E | P] (12 pivots over 24 lanes, 12-entry columns: 4x the v_readlane
+  // broadcasts).  lsolve's operators, in the original basis:
+  //   S L = T^T V^T G            (S_k B = (S L) B6: its only use of S_k),
+  //   M_k = A^T (I - S E) = (I + Nm^T / 2) (I - V^T Y [0 I]) (I + Nm^T / 2).
+  // S L and M_k are never formed from S: where E is large S is small in E's range and
+  // P~ - V^T Y V cancels there (absolute error eps |P|, then multiplied by E), while V^T G and
+  // V^T Y carry no such cancellation (tools/ipm_proto.py FACTOR=range: identical iteration counts
+  // on its 64 + 32 cases; S L taken from S fails a sparse N = 32 case).
+  auto nm12 = [&](int i, int j) -> double {   // Nm[i][j] on the 12-state
+    if (i < 3 && j >= 6 && j < 9) return sm.nmr[i][j - 6];
+    if (i >= 3 && i < 6 && j == i + 6) return h;
+    return 0.0;
+  };
+  double NbT[3], IpB[3];   // Nm[lc][4q + lr] (B operands of Nm^T); (I + Nm^T / 2)[4q + lr][lc]
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int c = 4 * q + lr;
+    const bool ok = c < 12 && lc < 12;
+    NbT[q] = ok ? nm12(lc, c) : 0.0;
+    IpB[q] = ok ? (c == lc ? 1.0 : 0.0) + 0.5 * nm12(lc, c) : 0.0;
+  }
+  {   // Qt = (I + Nm^T / 2) Qh (I + Nm / 2) -> sm.QT (once per robot)
+    const d4 Qr = qhat4();
+    d4 R = Qr;   // Qh (I + Nm / 2)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) R = mfma(Qr[q], 0.5 * Nmb[q], R);
+    d4 Q = R;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) Q = mfma(0.5 * Nmb[q], R[q], Q);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = lr + 4 * i;
+      if (r < 12 && lc < 12) sm.QT[12 * r + lc] = Q[i];
+    }
+    fsync<NT>();
+  }
+  auto qt4 = [&]() -> d4 {   // Qt in result layout
+    d4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = (lr + 4 * i < 12 && lc < 12) ? sm.QT[12 * (lr + 4 * i) + lc] : 0.0;
+    return v;
+  };
+  auto blk6 = [&](const d4& X, bool cols) -> d4 {   // rows 6..11 of X (and columns 6..11 when cols)
+    d4 c;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c[i] = (lr + 4 * i >= 6 && (!cols || lc >= 6)) ? X[i] : 0.0;
+    return c;
+  };
   constexpr bool kMG = IpmSharedT<NM, FULL, MG>::kMG;
-  auto stage_m = [&](int k, const d4& Sr, const d4& Er) {   // M_k = (I + Nm^T) (I - S E) -> M[k] (and M^T)
-    d4 Lr = diag4(1.0);
+  // M_k = (I + Nm^T / 2) X (I + Nm^T / 2), X = I - V^T Y [0 I] -> M[k] (and M^T).  Zr = (Y V)'s
+  // result registers: X^T = I - Y V, so its result registers are X's A operands
+  auto stage_m = [&](int k, const d4& Zr) {
+    d4 R1 = diag4(0.0);   // X (I + Nm^T / 2)
 #pragma unroll
-    for (int q = 0; q < 3; ++q) Lr = mfma(-Sr[q], Er[q], Lr);
-    d4 Mr = Lr;
+    for (int q = 0; q < 3; ++q) R1 = mfma(((lr + 4 * q == lc && lc < 12) ? 1.0 : 0.0) - Zr[q], IpB[q], R1);
+    d4 Mr = R1;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) Mr = mfma(Nmb[q], Lr[q], Mr);
+    for (int q = 0; q < 2; ++q) Mr = mfma(0.5 * Nmb[q], R1[q], Mr);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = lr + 4 * i;
@@ -575,79 +633,115 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     }
   };
 
+  // Riccati factorisation: per stage k the global slot's 144 doubles hold S_k L (12 x 6,
+  // row-major) and its transpose (6 x 12), lsolve's only uses of S_k; M_k as stage_m stores it
   auto factor = [&]() {
     IPM_T0();
-    d4 Pr = qhat4();
-    d4 Er = stage_e(N - 1), Sp = diag4(0.0), Ep = diag4(0.0);
-    const int jc = lane < 12 ? lane : (lane < 24 ? lane - 12 : 0);
+    d4 Pr = qt4();   // P~_{k+1}
+    d4 Cr = blk6(stage_e(N - 1), true), Zp = diag4(0.0);
+    const int jc = lane < 18 ? lane : 0;
     for (int k = N - 1; k >= 0; --k) {
       IPM_TS(ta);
-      d4 Tr = diag4(1.0);
+      const d4 Kr = blk6(Pr, true);
+      d4 Mr = diag4(1.0);   // I + C K
 #pragma unroll
-      for (int q = 0; q < 3; ++q) Tr = mfma(Pr[q], Er[q], Tr);
+      for (int q = 1; q < 3; ++q) Mr = mfma(Cr[q], Kr[q], Mr);
+      // column c < 6 of I + C K at TT[c], column c of C at TT[6 + c] (rows 6..11 -> 0..5)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = lr + 4 * i;
-        if (r < 12 && lc < 12) {
-          sm.TT[lc][r] = Tr[i];
-          sm.P[12 * r + lc] = Pr[i];
+        if (r >= 6 && r < 12 && lc >= 6 && lc < 12) {
+          sm.TT[lc - 6][r - 6] = Mr[i];
+          sm.TT[lc][r - 6] = Cr[i];
         }
       }
       fsync<NT>();
       IPM_TS(tb);
-      double col[12];
-      if (lane < 12) ld12(col, sm.TT[jc]);
-      else ld12(col, sm.P + 12 * jc);   // column jc of P = row jc (P symmetric)
-      // under the sweep: M of the previous stage, E of the next
-      if (k < N - 1) stage_m(k + 1, Sp, Ep);
-      const d4 En = k > 0 ? stage_e(k - 1) : diag4(0.0);
+      double col[6];   // lanes 0..5: I + C K, 6..11: C, 12..17: I
+      if (lane < 12) {
+        const d2* q = reinterpret_cast<const d2*>(sm.TT[jc]);
 #pragma unroll
-      for (int kk = 0; kk < 12; ++kk) {
-        double pc[12];
+        for (int i = 0; i < 3; ++i) {
+          const d2 x = q[i];
+          col[2 * i] = x[0];
+          col[2 * i + 1] = x[1];
+        }
+      } else {
 #pragma unroll
-        for (int i = 0; i < 12; ++i) pc[i] = readlane_d(col[i], kk);
+        for (int i = 0; i < 6; ++i) col[i] = jc - 12 == i ? 1.0 : 0.0;
+      }
+      // under the sweep: M of the previous stage, C of the next
+      if (k < N - 1) stage_m(k + 1, Zp);
+      const d4 Cn = k > 0 ? blk6(stage_e(k - 1), true) : diag4(0.0);
+#pragma unroll
+      for (int kk = 0; kk < 6; ++kk) {
+        double pc[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) pc[i] = readlane_d(col[i], kk);
         const double ip = rcp_nr(pc[kk]);
         const double rowv = col[kk] * ip;
 #pragma unroll
-        for (int i = 0; i < 12; ++i) col[i] = (i == kk) ? rowv : fma(-pc[i], rowv, col[i]);
+        for (int i = 0; i < 6; ++i) col[i] = (i == kk) ? rowv : fma(-pc[i], rowv, col[i]);
       }
       IPM_TS(tc);
-      if (lane >= 12 && lane < 24) st12(sm.TT[jc], col);   // S^T row jc = column jc of S
+      if (lane >= 6 && lane < 18) {   // Y's columns over C's (TT[6 + c]), G's over I + C K's (TT[c])
+        d2* q = reinterpret_cast<d2*>(sm.TT[lane < 12 ? jc : jc - 12]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) q[i] = d2{col[2 * i], col[2 * i + 1]};
+      }
       fsync<NT>();
       IPM_TS(td);
       IPM_TA(4, ta, tb);
       IPM_TA(5, tb, tc);
       IPM_TA(6, tc, td);
-      d4 Sr;   // S_k = (S + S^T) / 2, kept for lsolve
+      d4 Yr, Gr;   // (Y + Y^T) / 2 and G in the block [6:12, 6:12]
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = lr + 4 * i;
-        double v = 0.0;
-        if (r < 12 && lc < 12) {
-          v = 0.5 * (sm.TT[lc][r] + sm.TT[r][lc]);
-          Sg[k * 144 + 12 * r + lc] = v;
-        }
-        Sr[i] = v;
+        const bool in = r >= 6 && r < 12 && lc >= 6 && lc < 12;
+        const int r6 = in ? r - 6 : 0, c6 = in ? lc - 6 : 0;
+        Yr[i] = in ? 0.5 * (sm.TT[6 + c6][r6] + sm.TT[6 + r6][c6]) : 0.0;
+        Gr[i] = in ? sm.TT[c6][r6] : 0.0;
       }
-      if (k > 0) {   // P_k = Qh + (I + Nm^T) S (I + Nm)
+      const d4 Vr = blk6(Pr, false);
+      d4 Zr = diag4(0.0);   // Y V
+#pragma unroll
+      for (int q = 1; q < 3; ++q) Zr = mfma(Yr[q], Vr[q], Zr);
+      if (k > 0) {   // P~_k = Qt + A^T S~ A, S~ = P~ - V^T Y V
+        d4 Sr = Pr;
+#pragma unroll
+        for (int q = 1; q < 3; ++q) Sr = mfma(-Vr[q], Zr[q], Sr);
         d4 SA = Sr;
 #pragma unroll
         for (int q = 0; q < 2; ++q) SA = mfma(Sr[q], Nmb[q], SA);
-        Pr = qhat4();
+        Pr = qt4();
 #pragma unroll
         for (int i = 0; i < 4; ++i) Pr[i] += SA[i];
 #pragma unroll
         for (int q = 0; q < 2; ++q) Pr = mfma(Nmb[q], SA[q], Pr);
       }
-      Sp = Sr;
-      Ep = Er;
-      Er = En;
+      d4 SLt = diag4(0.0);   // S~ [0; I] = V^T G (columns 6..11)
+#pragma unroll
+      for (int q = 1; q < 3; ++q) SLt = mfma(Vr[q], Gr[q], SLt);
+      d4 SLr = SLt;   // S L = T^T S~ [0; I] = (I - Nm^T / 2) V^T G
+#pragma unroll
+      for (int q = 0; q < 2; ++q) SLr = mfma(-0.5 * Nmb[q], SLt[q], SLr);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = lr + 4 * i;
+        if (r < 12 && lc >= 6 && lc < 12) {
+          Sg[k * 144 + 6 * r + lc - 6] = SLr[i];
+          Sg[k * 144 + 72 + 12 * (lc - 6) + r] = SLr[i];
+        }
+      }
+      Zp = Zr;
+      Cr = Cn;
       IPM_TS(te);
       IPM_TA(7, td, te);
     }
-    stage_m(0, Sp, Ep);
-    fsync<NT>();   // S_k, M_k for lsolve
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // the global stores (S_k, M_k), before lsolve reads them
+    stage_m(0, Zp);
+    fsync<NT>();   // S_k L, M_k for lsolve
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // the global stores (S_k L, M_k), before lsolve reads them
     IPM_T1(1);
   };
 
@@ -686,13 +780,14 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
   };
   double btop[3];   // B_d^T's operands for the lsolve phases
   bt_ops(btop);
-  auto smat = [&](double (*dst)[NU], double (*src)[NU]) {   // dst_k = S_k src_k, every stage
+  // dst_k = S_k src_k for src_k = B_d y in B_d's range, every stage: (S_k L) (src_k rows 6..11)
+  auto smat = [&](double (*dst)[NU], double (*src)[NU]) {
     for (int e = lane; e < N * NU; e += NT) {
       const int k = e / NU, i = e % NU;
-      double sr[12], v[12];
-      ld12g(sr, Sg + k * 144 + 12 * i);
-      ld12(v, src[k]);
-      dst[k][i] = dot12(sr, v);
+      const d2* sr = reinterpret_cast<const d2*>(Sg + k * 144 + 6 * i);
+      const d2* v = reinterpret_cast<const d2*>(src[k] + 6);
+      const d2 s0 = sr[0], s1 = sr[1], s2 = sr[2], v0 = v[0], v1 = v[1], v2 = v[2];
+      dst[k][i] = fma(s0[0], v0[0], fma(s1[0], v1[0], s2[0] * v2[0])) + fma(s0[1], v0[1], fma(s1[1], v1[1], s2[1] * v2[1]));
     }
     fsync<NT>();
   };
@@ -803,23 +898,27 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       }
     }
     fsync<NT>();
-    for (int e = lane; e < N * NU; e += NT) {   // la_k = S_k (B Y_k - A dx_k)
+    for (int e = lane; e < N * NU; e += NT) {   // la_k = L^T S_k (B Y_k - A dx_k) at rows 6..11, 0 above
       const int k = e / NU, i = e % NU;
-      double dxv[12], by[12], sr[12];
-      ld12(dxv, sm.dxh[k]);
-      ld12(by, sm.By[k]);
-      ld12g(sr, Sg + k * 144 + 12 * i);
+      double v = 0.0;
+      if (i >= 6) {
+        double dxv[12], by[12], sr[12];
+        ld12(dxv, sm.dxh[k]);
+        ld12(by, sm.By[k]);
+        ld12g(sr, Sg + k * 144 + 72 + 12 * (i - 6));   // row i - 6 of (S_k L)^T
 #pragma unroll
-      for (int m = 0; m < 12; ++m) {   // A dx on the 12-state
-        double a = dxv[m];
-        if (m < 3) a += sm.nmr[m][0] * dxv[6] + sm.nmr[m][1] * dxv[7] + sm.nmr[m][2] * dxv[8];
-        else if (m < 6) a += h * dxv[m + 6];
-        by[m] -= a;
+        for (int m = 0; m < 12; ++m) {   // A dx on the 12-state
+          double a = dxv[m];
+          if (m < 3) a += sm.nmr[m][0] * dxv[6] + sm.nmr[m][1] * dxv[7] + sm.nmr[m][2] * dxv[8];
+          else if (m < 6) a += h * dxv[m + 6];
+          by[m] -= a;
+        }
+        v = dot12(sr, by);
       }
-      sm.la[k][i] = dot12(sr, by);
+      sm.la[k][i] = v;
     }
     fsync<NT>();
-    stage_gemm(sm.lb, sm.la, btop);   // B^T la_k (lb is dead after B lb)
+    stage_gemm(sm.lb, sm.la, btop);   // B^T S_k (...) = B6^T la_k[6:12] (lb is dead after B lb)
     for (int e = lane; e < N * NU; e += NT) {   // d_k = W_k B^T la_k - Y_k
       const int k = e / NU, c = e % NU;
       sm.dU[k][c] = wz(k, c, sm.lb, nullptr) - sm.Y[k][c];

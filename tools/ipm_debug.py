@@ -24,8 +24,11 @@ from helpers import rel_err_u0  # noqa: E402
 
 N = int(os.environ.get("N", "16"))
 cases = [int(c) for c in os.environ.get("CASES", "5,6,15").split(",")]
+FLEET = int(os.environ.get("FLEET", "0"))   # > 0: that many robots (the cases repeated), mean cycles only
 z = np.load(os.path.join(ROOT, "tests", "golden", f"formulation_N{N}.npz"), allow_pickle=False)
 bt = {k: z[k][cases] for k in ("x0", "xref", "contact", "feet", "robot")}
+if FLEET:
+    bt = {k: np.concatenate([v] * (FLEET // len(cases) + 1))[:FLEET] for k, v in bt.items()}
 # debug build: same call through the diagnostic library
 lib = ctypes.CDLL(DBG)
 params = _lib.MpcqpParams()
@@ -48,6 +51,13 @@ rc = lib.mpcqp_solve(ctx, B, p(t["x0"]), p(t["xref"]), p(t["contact"]), p(t["fee
 torch.cuda.synchronize()
 assert rc == 0, rc
 D = Ud.cpu().numpy()
+if FLEET:
+    cyc = D[:, N * 12 - 8:].astype(np.float64)
+    print(f"fleet of {FLEET} ({len(cases)} cases repeated): mean cycles per robot: gradient {cyc[:, 0].mean():.3g} "
+          f"factor {cyc[:, 1].mean():.3g} lsolve {cyc[:, 2].mean():.3g} total {cyc[:, 3].mean():.3g}; factor T "
+          f"{cyc[:, 4].mean():.3g} GJ {cyc[:, 5].mean():.3g} S store {cyc[:, 6].mean():.3g} sym {cyc[:, 7].mean():.3g}; "
+          f"factorisations mean {itd.cpu().numpy().mean():.2f}")
+    sys.exit(0)
 for i, c in enumerate(cases):
     print(f"--- case {c} trace (it, mu, polish stat/g, slack min, lam min, nfact, gscale, hscale)")
     cyc = D[i][N * 12 - 8:]

@@ -40,6 +40,7 @@ EARLY_MAXV = int(os.environ.get("EARLY_MAXV", "1000000"))  # only when the start
 EARLY = int(os.environ.get("EARLY", "-1"))              # >= 0: polish from the start point's violated
                                                         # rows first, with this many corrections
 MAX_IT = int(os.environ.get("MAX_IT", "60"))
+FACTOR = os.environ.get("FACTOR", "info")               # "range": S on B_d's 6-dimensional range
 
 
 def cone(mu, normal):
@@ -89,6 +90,12 @@ def solve(Ad, Bd, x0, xref, contact, N, mu, fz_max, normal, q_diag=F.Q_DIAG, r_d
     for (k, leg) in feet:
         stance[k, leg] = True
     m_tot = nf * R
+    # B = Lr B[6:12] (13 x 6): the kernel's B_d is rank 6 to rounding (its rows 0..5 are
+    # (h / 2) R_z^T K and h / 2m, formed from rows 6..11); the oracle's float32 B_d to ~1e-9,
+    # so both forms below run on the projected B
+    Lr = B @ np.linalg.pinv(B[6:12])
+    solve.lres = float(np.abs(B - Lr @ B[6:12]).max() / np.abs(B).max())
+    B = Lr @ B[6:12]
     Bleg = np.stack([B[:, 3 * l:3 * l + 3] for l in range(4)])   # (4, 13, 3)
 
     def fview(U):
@@ -118,19 +125,33 @@ def solve(Ad, Bd, x0, xref, contact, N, mu, fz_max, normal, q_diag=F.Q_DIAG, r_d
 
     def factor(Bl, Ri):
         cnt["factor"] += 1
-        """S_k = (I + P_{k+1} E_k)^-1 P_{k+1}; Bl (N,4,13,3), Ri (N,4,3,3)."""
+        """S_k = (I + P_{k+1} E_k)^-1 P_{k+1}; Bl (N,4,13,3), Ri (N,4,3,3).  FACTOR=range also
+        returns S_k L (13 x 6): the Newton solve takes S only as S B = S L B6, accurate in that
+        form (S = P - V^T Y V cancels where E is large; S L = V^T (I + C K)^-1 does not)."""
         S = np.zeros((N, 13, 13))
+        SL = np.zeros((N, 13, 6))
         P = np.diag(Qh)
         for k in range(N - 1, -1, -1):
-            E = sum(Bl[k, l] @ Ri[k, l] @ Bl[k, l].T for l in range(4))
-            S[k] = gj_inverse(np.eye(13) + P @ E) @ P
+            if FACTOR == "range":   # B_d = L B6 (B6 = rows 6..11): E = L C L^T, C = B6 W B6^T (6 x 6)
+                C = sum(Bl[k, l][6:12] @ Ri[k, l] @ Bl[k, l][6:12].T for l in range(4))
+                V = Lr.T @ P
+                Kr = V @ Lr
+                G6 = gj_inverse(np.eye(6) + C @ Kr)
+                Y = G6 @ C
+                S[k] = P - V.T @ Y @ V
+                SL[k] = V.T @ G6
+            else:
+                E = sum(Bl[k, l] @ Ri[k, l] @ Bl[k, l].T for l in range(4))
+                S[k] = gj_inverse(np.eye(13) + P @ E) @ P
+                SL[k] = S[k] @ Lr
             S[k] = 0.5 * (S[k] + S[k].T)
             P = np.diag(Qh) + A.T @ S[k] @ A
-        return S
+        return SL
 
-    def lsolve(Bl, Ri, S, rhs):
+    def lsolve(Bl, Ri, SL, rhs):
         cnt["lsolve"] += 1
-        """(H + per-leg Rt - Rh) d = rhs on the legs' subspaces (Bl already projected)."""
+        """(H + per-leg Rt - Rh) d = rhs on the legs' subspaces (Bl already projected); S_k
+        enters as S_k L only: S B y = (S L) (B y)[6:12], L^T S v = (S L)^T v."""
         p = np.zeros(13)
         Y = np.zeros((N, 4, 3))
         for k in range(N - 1, -1, -1):
@@ -138,14 +159,14 @@ def solve(Ad, Bd, x0, xref, contact, N, mu, fz_max, normal, q_diag=F.Q_DIAG, r_d
                 Y[k, l] = Ri[k, l] @ (-rhs[k, 3 * l:3 * l + 3] + Bl[k, l].T @ p)
             By = sum(Bl[k, l] @ Y[k, l] for l in range(4))
             if k > 0:
-                p = A.T @ (p - S[k] @ By)
+                p = A.T @ (p - SL[k] @ By[6:12])
         d = np.zeros((N, 12))
         dx = np.zeros(13)
         for k in range(N):
             By = sum(Bl[k, l] @ Y[k, l] for l in range(4))
-            w = S[k] @ (By - A @ dx)
+            w = SL[k].T @ (By - A @ dx)   # L^T S (B Y - A dx)
             for l in range(4):
-                d[k, 3 * l:3 * l + 3] = Ri[k, l] @ (Bl[k, l].T @ w) - Y[k, l]
+                d[k, 3 * l:3 * l + 3] = Ri[k, l] @ (Bl[k, l][6:12].T @ w) - Y[k, l]
             dx = A @ dx + sum(Bl[k, l] @ d[k, 3 * l:3 * l + 3] for l in range(4))
         return d
 
@@ -321,7 +342,7 @@ def main():
             worst = max(worst, eU)
             iters.append(it)
             fails += not ok
-            print(f"{name} b={b:2d} stance={nf:2d} it={it:2d} ok={int(ok)} err u0 {e0:.2e} U {eU:.2e}")
+            print(f"{name} b={b:2d} stance={nf:2d} it={it:2d} ok={int(ok)} err u0 {e0:.2e} U {eU:.2e} Lres {solve.lres:.1e}")
     print(f"worst {worst:.2e}  iterations mean {np.mean(iters):.1f} max {max(iters)}  unverified {fails}")
 
 
