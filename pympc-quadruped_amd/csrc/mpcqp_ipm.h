@@ -1190,6 +1190,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
 
   // ------------------------------------------------ interior point
   int it = 0;
+  double ap_last = 0.0, ad_last = 0.0;   // the last step's lengths (FDS / FDL hold its direction); 0: none yet
   while (!done && it < IPM_MAX_IT) {
     ++it;
     gradient();
@@ -1230,7 +1231,15 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
         int a = 0;
 #pragma unroll
         for (int r = 0; r < 6; ++r)
-          if (((liv >> r) & 1) && FL(j)[r] > FS(j)[r]) a |= 1 << r;
+          if ((liv >> r) & 1) {
+            // the rows whose slack the last step shrank by a larger factor than their
+            // multiplier (Tapia's indicator: lam+ / lam > s+ / s; lam > s before any step) --
+            // lam > s misses the weakly active rows, whose lam is still below s at this mu
+            // (tools/ipm_proto.py POLISH_RULE=tapia: 13.1 -> 10.6 factorisations per robot)
+            const double s1 = FS(j)[r], l1 = FL(j)[r];
+            const double s0 = s1 - ap_last * FDS(j)[r], l0 = l1 - ad_last * FDL(j)[r];
+            if (ap_last > 0.0 ? l1 * s0 > s1 * l0 : l1 > s1) a |= 1 << r;
+          }
         FACT(j) = a;
       }
       // U is overwritten by the polish: keep the IPM iterate
@@ -1317,6 +1326,8 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     fsync<NT>();
     al = newton(true, target);
     const double ap = fmin(1.0, IPM_TAU * al[0]), ad = fmin(1.0, IPM_TAU * al[1]);
+    ap_last = ap;
+    ad_last = ad;
     for (int j = lane; j < S; j += NT) {
       double d[3];
       foot(j, sm.dU, d);

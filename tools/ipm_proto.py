@@ -40,6 +40,9 @@ EARLY_MAXV = int(os.environ.get("EARLY_MAXV", "1000000"))  # only when the start
 EARLY = int(os.environ.get("EARLY", "-1"))              # >= 0: polish from the start point's violated
                                                         # rows first, with this many corrections
 MAX_IT = int(os.environ.get("MAX_IT", "60"))
+# polish set: "ratio" lam > s; "tapia": the last step's lam_new / lam_old > s_new / s_old (an
+# active row's slack shrinks faster than its multiplier, an inactive row's multiplier faster)
+POLISH_RULE = os.environ.get("POLISH_RULE", "ratio")
 FACTOR = os.environ.get("FACTOR", "info")               # "range": S on B_d's 6-dimensional range
 
 
@@ -263,6 +266,7 @@ def solve(Ad, Bd, x0, xref, contact, N, mu, fz_max, normal, q_diag=F.Q_DIAG, r_d
     s = np.maximum(fview(U) @ G.T - h, 1.0)
     lam = np.ones((nf, R))
     polish_tries = 0
+    s_prev, lam_prev = None, None
     for it in range(1, MAX_IT + 1):
         rd = gradient(U) - gt(lam)
         rp = fview(U) @ G.T - h - s
@@ -271,7 +275,10 @@ def solve(Ad, Bd, x0, xref, contact, N, mu, fz_max, normal, q_diag=F.Q_DIAG, r_d
             print(f"it {it:2d} rd {np.abs(rd).max():.2e} rp {np.abs(rp).max():.2e} mu {mu_c:.2e}")
         if mu_c < POLISH_MU * gscale * hscale:
             polish_tries += 1
-            act = lam > s
+            if POLISH_RULE == "tapia" and s_prev is not None:
+                act = lam / lam_prev > s / s_prev
+            else:
+                act = lam > s
             for corr in range(NCORR + 1):
                 u, info, nact = polish(act)
                 if verbose:
@@ -299,6 +306,7 @@ def solve(Ad, Bd, x0, xref, contact, N, mu, fz_max, normal, q_diag=F.Q_DIAG, r_d
         ap = min(1.0, TAU * _max_step(s, ds))
         ad = min(1.0, TAU * _max_step(lam, dl))
         U = U + ap * dU
+        s_prev, lam_prev = s, lam
         s = s + ap * ds
         lam = lam + ad * dl
     solve.cnt = cnt
@@ -322,7 +330,7 @@ def run_case(bt, b, N, verbose=False):
 
 
 def main():
-    worst, iters, fails = 0.0, [], 0
+    worst, iters, fails, nfac = 0.0, [], 0, []
     cases = []
     for N in (10, 16, 20):
         z = np.load(os.path.join(ROOT, "tests", "golden", f"formulation_N{N}.npz"), allow_pickle=False)
@@ -342,8 +350,11 @@ def main():
             worst = max(worst, eU)
             iters.append(it)
             fails += not ok
-            print(f"{name} b={b:2d} stance={nf:2d} it={it:2d} ok={int(ok)} err u0 {e0:.2e} U {eU:.2e} Lres {solve.lres:.1e}")
-    print(f"worst {worst:.2e}  iterations mean {np.mean(iters):.1f} max {max(iters)}  unverified {fails}")
+            nfac.append(solve.cnt["factor"])
+            print(f"{name} b={b:2d} stance={nf:2d} it={it:2d} factor={solve.cnt['factor']:2d} ok={int(ok)} "
+                  f"err u0 {e0:.2e} U {eU:.2e} Lres {solve.lres:.1e}")
+    print(f"worst {worst:.2e}  iterations mean {np.mean(iters):.1f} max {max(iters)}  factorisations mean "
+          f"{np.mean(nfac):.2f} max {max(nfac)}  unverified {fails}")
 
 
 if __name__ == "__main__":
