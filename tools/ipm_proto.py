@@ -248,8 +248,19 @@ def solve(Ad, Bd, x0, xref, contact, N, mu, fz_max, normal, q_diag=F.Q_DIAG, r_d
     gscale = 1.0 + np.abs(g0).max()
     hscale = 1.0 + np.abs(h).max()
     # start: minimiser under a mild barrier weight, slacks shifted into the interior
-    Bl, Ri = ipm_blocks(np.full((nf, R), 1e-2))
-    U = lsolve(Bl, Ri, factor(Bl, Ri), -g0)
+    START = os.environ.get("START", "barrier")
+    if START == "barrier":
+        Bl, Ri = ipm_blocks(np.full((nf, R), 1e-2))
+        U = lsolve(Bl, Ri, factor(Bl, Ri), -g0)
+    elif START == "gravity":   # each stance foot carries m g / (stance feet at its stage), vertically
+        mg = 9.81 * A[3, 9] / B[9, 0]   # A_d[3][9] = h, B_d[9][0] = h / m
+        U = np.zeros((N, 12))
+        for k in range(N):
+            legs = [l for l in range(4) if stance[k, l]]
+            for l in legs:
+                U[k, 3 * l + 2] = mg / len(legs)
+    else:
+        U = np.zeros((N, 12))
     act = (fview(U) @ G.T - h) < 0
     solve.nviol = int(act.sum())
     if EARLY >= 0 and solve.nviol <= EARLY_MAXV:
