@@ -37,8 +37,10 @@ constexpr int IPM_NCORR = 8;
 constexpr int IPM_NREF = 2;
 constexpr double IPM_TAU = 0.995;
 // polish once mu < this * scale (tools/ipm_ab.sh: 1e-7 -> 3e-9 cut the slowest of 256 standing
-// robots from 31 to 18 factorisations)
-constexpr double IPM_POLISH_MU = 3e-9;
+// robots from 31 to 18 factorisations; round 6, with the Tapia polish set, 3e-9 -> 5e-10: a
+// first polish that verifies more often, standing fleet 0.724 -> 0.753 M QP/s though the mean
+// factorisations rise 10.64 -> 10.86; 1e-8 / 3e-8 slower, profiles/r6_ipm/polish_mu.txt)
+constexpr double IPM_POLISH_MU = 5e-10;
 constexpr double IPM_MU_FLOOR = 1e-13;
 constexpr double IPM_STAT_TOL = 1e-10;
 constexpr int IPM_FPL = 2;             // stance foot-steps per lane (4 kMaxN <= 128)
