@@ -635,8 +635,9 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     }
   };
 
-  // Riccati factorisation: per stage k the global slot's 144 doubles hold S_k L (12 x 6,
-  // row-major) and its transpose (6 x 12), lsolve's only uses of S_k; M_k as stage_m stores it
+  // Riccati factorisation: per stage k the global slot's 144 doubles hold S~_k [0; I] = V^T G
+  // (12 x 6, row-major) and its transpose (6 x 12), from which lsolve takes every product with
+  // S_k (S_k L = T^T V^T G); M_k as stage_m stores it
   auto factor = [&]() {
     IPM_T0();
     d4 Pr = qt4();   // P~_{k+1}
@@ -722,12 +723,9 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
 #pragma unroll
         for (int q = 0; q < 2; ++q) Pr = mfma(Nmb[q], SA[q], Pr);
       }
-      d4 SLt = diag4(0.0);   // S~ [0; I] = V^T G (columns 6..11)
+      d4 SLr = diag4(0.0);   // S~ [0; I] = V^T G (columns 6..11); lsolve applies S L = T^T of it
 #pragma unroll
-      for (int q = 1; q < 3; ++q) SLt = mfma(Vr[q], Gr[q], SLt);
-      d4 SLr = SLt;   // S L = T^T S~ [0; I] = (I - Nm^T / 2) V^T G
-#pragma unroll
-      for (int q = 0; q < 2; ++q) SLr = mfma(-0.5 * Nmb[q], SLt[q], SLr);
+      for (int q = 1; q < 3; ++q) SLr = mfma(Vr[q], Gr[q], SLr);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = lr + 4 * i;
@@ -782,14 +780,17 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
   };
   double btop[3];   // B_d^T's operands for the lsolve phases
   bt_ops(btop);
-  // dst_k = S_k src_k for src_k = B_d y in B_d's range, every stage: (S_k L) (src_k rows 6..11)
-  auto smat = [&](double (*dst)[NU], double (*src)[NU]) {
+  // t_k = S~_k [0; I] (src_k rows 6..11) for src_k = B_d y in B_d's range, every stage, so that
+  // S_k src_k = T^T t_k; range: rows 0..5 of t_k set to 0 (then B_d^T T^T t_k = B_d^T dst_k,
+  // T B_d = [0; B6])
+  auto smat = [&](double (*dst)[NU], double (*src)[NU], bool range) {
     for (int e = lane; e < N * NU; e += NT) {
       const int k = e / NU, i = e % NU;
       const d2* sr = reinterpret_cast<const d2*>(Sg + k * 144 + 6 * i);
       const d2* v = reinterpret_cast<const d2*>(src[k] + 6);
       const d2 s0 = sr[0], s1 = sr[1], s2 = sr[2], v0 = v[0], v1 = v[1], v2 = v[2];
-      dst[k][i] = fma(s0[0], v0[0], fma(s1[0], v1[0], s2[0] * v2[0])) + fma(s0[1], v0[1], fma(s1[1], v1[1], s2[1] * v2[1]));
+      const double t = fma(s0[0], v0[0], fma(s1[0], v1[0], s2[0] * v2[0])) + fma(s0[1], v0[1], fma(s1[1], v1[1], s2[1] * v2[1]));
+      dst[k][i] = range && i < 6 ? 0.0 : t;
     }
     fsync<NT>();
   };
@@ -811,12 +812,12 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     }
     fsync<NT>();
     bmat(sm.lb, sm.la);   // B W rhs
-    smat(sm.la, sm.lb);   // S B W rhs
-    for (int e = lane; e < N * NU; e += NT) {   // lc_k = A^T la_k
+    smat(sm.la, sm.lb, false);   // t: S B W rhs = T^T t
+    for (int e = lane; e < N * NU; e += NT) {   // lc_k = A^T S B W rhs = A^T T^T t = (I + Nm / 2)^T t
       const int k = e / NU, i = e % NU;
       double v = sm.la[k][i];
-      if (i >= 6 && i < 9) v += sm.nmr[0][i - 6] * sm.la[k][0] + sm.nmr[1][i - 6] * sm.la[k][1] + sm.nmr[2][i - 6] * sm.la[k][2];
-      else if (i >= 9) v += h * sm.la[k][i - 6];
+      if (i >= 6 && i < 9) v += 0.5 * (sm.nmr[0][i - 6] * sm.la[k][0] + sm.nmr[1][i - 6] * sm.la[k][1] + sm.nmr[2][i - 6] * sm.la[k][2]);
+      else if (i >= 9) v += 0.5 * h * sm.la[k][i - 6];
       sm.lc[k][i] = v;
     }
     fsync<NT>();
@@ -859,7 +860,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     }
     fsync<NT>();
     bmat(sm.By, sm.Y);    // B Y
-    smat(sm.la, sm.By);   // S B Y
+    smat(sm.la, sm.By, true);   // [0; t rows 6..11]: B^T of it = B^T S B Y
     stage_gemm(sm.lc, sm.la, btop);   // B^T S B Y (lc is dead until B lb below)
     for (int e = lane; e < N * NU; e += NT) {   // lb_k = W_k B^T S_k B Y_k - Y_k
       const int k = e / NU, c = e % NU;
@@ -900,14 +901,14 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       }
     }
     fsync<NT>();
-    for (int e = lane; e < N * NU; e += NT) {   // la_k = L^T S_k (B Y_k - A dx_k) at rows 6..11, 0 above
+    for (int e = lane; e < N * NU; e += NT) {   // la_k = L^T S_k (B Y_k - A dx_k) = (V^T G)^T T (...) at rows 6..11, 0 above
       const int k = e / NU, i = e % NU;
       double v = 0.0;
       if (i >= 6) {
         double dxv[12], by[12], sr[12];
         ld12(dxv, sm.dxh[k]);
         ld12(by, sm.By[k]);
-        ld12g(sr, Sg + k * 144 + 72 + 12 * (i - 6));   // row i - 6 of (S_k L)^T
+        ld12g(sr, Sg + k * 144 + 72 + 12 * (i - 6));   // row i - 6 of (V^T G)^T
 #pragma unroll
         for (int m = 0; m < 12; ++m) {   // A dx on the 12-state
           double a = dxv[m];
@@ -915,6 +916,9 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
           else if (m < 6) a += h * dxv[m + 6];
           by[m] -= a;
         }
+#pragma unroll
+        for (int m = 0; m < 6; ++m)   // T (B Y - A dx): (S L)^T v = (V^T G)^T T v
+          by[m] -= 0.5 * (m < 3 ? sm.nmr[m][0] * by[6] + sm.nmr[m][1] * by[7] + sm.nmr[m][2] * by[8] : h * by[m + 6]);
         v = dot12(sr, by);
       }
       sm.la[k][i] = v;
