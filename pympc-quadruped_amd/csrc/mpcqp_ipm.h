@@ -26,14 +26,20 @@
 //     the null spaces, primal feasibility of every row and multipliers >= 0 (the
 //     gradient in the cone of the foot's active rows, Caratheodory subsets).  A failed
 //     check corrects the set (violated rows in, the most negative multiplier out) up
-//     to IPM_NCORR times; the IPM continues otherwise.
+//     to IPM_NCORR times (IPM_NCORR_IPM from an interior-point iterate); the IPM continues
+//     otherwise.
 // A verified polish is the exact optimum (status OK); tools/ipm_proto.py is the NumPy
 // model of every step (64 golden / synthetic cases, worst error 1.3e-6).
 
 #include "mpcqp_ipm_foot.h"
 
 constexpr int IPM_MAX_IT = 60;
-constexpr int IPM_NCORR = 8;
+constexpr int IPM_NCORR = 8;       // set corrections of a warm start's polish
+// ... and of a polish from an interior-point iterate: a set that needs more is far off, and one
+// more IPM iteration (one factorisation) costs less than the corrections (one each): round 6,
+// tools/ipm_proto.py NCORR=2 -- the slowest standing robots 22 -> 16 factorisations, the
+// golden / synthetic cases unchanged (mean 10.95, max 13)
+constexpr int IPM_NCORR_IPM = 2;
 constexpr int IPM_NREF = 2;
 constexpr double IPM_TAU = 0.995;
 // polish once mu < this * scale (tools/ipm_ab.sh: 1e-7 -> 3e-9 cut the slowest of 256 standing
@@ -1124,9 +1130,9 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     return stat < IPM_STAT_TOL * gscale && smin > -tol_h && lminw > -tol_g;
   };
   // polish, then correct the set (violated rows in, the most negative multiplier out)
-  // until it verifies, stops changing or IPM_NCORR corrections are spent
-  auto polish_corrected = [&]() -> bool {
-    for (int corr = 0; corr <= IPM_NCORR; ++corr) {
+  // until it verifies, stops changing or ncorr corrections are spent
+  auto polish_corrected = [&](int ncorr) -> bool {
+    for (int corr = 0; corr <= ncorr; ++corr) {
       int changed = 0;
       for (int j = lane; j < S; j += NT) FPREV(j) = FACT(j);
       fsync<NT>();
@@ -1149,7 +1155,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       known |= v & 0x80;
     }
     if (__any(known)) {
-      if (polish_corrected()) {
+      if (polish_corrected(IPM_NCORR)) {
         done = true;
         status = MPCQP_STATUS_OK;
       } else {   // back to U = 0 and its gradient for the cold start
@@ -1254,7 +1260,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
         else sm.us.Us[e / NU][e % NU] = sm.U[e / NU][e % NU];
       }
       fsync<NT>();
-      if (polish_corrected()) {
+      if (polish_corrected(IPM_NCORR_IPM)) {
         done = true;
         status = MPCQP_STATUS_OK;
         break;

@@ -1,7 +1,8 @@
 """Diagnostic: solve one seeded batch with the library named by MPCQP_LIB and save
 u0 / iterations / status (compare two libraries with two runs):
   MPCQP_LIB=tools/libB.so python tools/lib_compare.py out.npz [B] [N] [gaits]
-(LC_RANGE=lo,hi: promise the stance range, e.g. 64,64 for an all-standing N = 16 fleet)"""
+(LC_RANGE=lo,hi: promise the stance range, e.g. 64,64 for an all-standing N = 16 fleet;
+LC_STAND=1: every robot standing)"""
 import os
 import sys
 
@@ -21,11 +22,14 @@ def main():
     N = int(sys.argv[3]) if len(sys.argv) > 3 else 10
     gaits = tuple(sys.argv[4].split(",")) if len(sys.argv) > 4 else ("trot10",)
     bt = make_batch(B, N, seed=1000, gaits=gaits, robots=("a1",))
+    if os.environ.get("LC_STAND"):
+        bt["contact"][:] = 1.0
     eng = LinearMpc(horizon=N, robot="a1", device="cuda:0")
     if os.environ.get("LC_RANGE"):   # "lo,hi": the caller's stance range (e.g. an all-standing fleet)
         eng.set_stance_range(*[int(v) for v in os.environ["LC_RANGE"].split(",")])
     res = eng.solve(bt["x0"], bt["xref"], bt["contact"], bt["feet"], robot=bt["robot"], return_all=True)
     torch.cuda.synchronize()
+    print("iterations histogram", np.bincount(res.iterations.cpu().numpy()).tolist())
     np.savez(out, u0=res.u0.cpu().numpy(), it=res.iterations.cpu().numpy(), st=res.status.cpu().numpy(),
              U=res.U.cpu().numpy())
     if len(sys.argv) > 5:
