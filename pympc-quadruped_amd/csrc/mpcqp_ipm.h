@@ -41,7 +41,10 @@ constexpr int IPM_NCORR = 8;       // set corrections of a warm start's polish
 // golden / synthetic cases unchanged (mean 10.95, max 13)
 constexpr int IPM_NCORR_IPM = 2;
 constexpr int IPM_NREF = 2;
-constexpr double IPM_TAU = 0.995;
+// fraction to the boundary (round 6: 0.995 -> 0.98 -- the slowest standing robots' long runs
+// of short steps end sooner: fleet factorisations mean 10.86 -> 10.32, max 19 -> 15, 0.79 ->
+// 0.935 M QP/s; 0.99 0.90 M, 0.97 0.93 M; tools/ipm_proto.py TAU: 64 cases all verified)
+constexpr double IPM_TAU = 0.98;
 // polish once mu < this * scale (tools/ipm_ab.sh: 1e-7 -> 3e-9 cut the slowest of 256 standing
 // robots from 31 to 18 factorisations; round 6, with the Tapia polish set, 3e-9 -> 5e-10: a
 // first polish that verifies more often, standing fleet 0.724 -> 0.753 M QP/s though the mean
