@@ -43,6 +43,7 @@ MAX_IT = int(os.environ.get("MAX_IT", "60"))
 # polish set: "ratio" lam > s; "tapia": the last step's lam_new / lam_old > s_new / s_old (an
 # active row's slack shrinks faster than its multiplier, an inactive row's multiplier faster)
 POLISH_RULE = os.environ.get("POLISH_RULE", "ratio")
+SIGMA_POW = float(os.environ.get("SIGMA_POW", "3"))    # Mehrotra's centring sigma = (mu_aff / mu)^this
 FACTOR = os.environ.get("FACTOR", "info")               # "range": S on B_d's 6-dimensional range
 
 
@@ -312,7 +313,7 @@ def solve(Ad, Bd, x0, xref, contact, N, mu, fz_max, normal, q_diag=F.Q_DIAG, r_d
         dU, ds, dl = newton(-s * lam)
         ap, ad = _max_step(s, ds), _max_step(lam, dl)
         mu_aff = float(((s + ap * ds) * (lam + ad * dl)).sum() / m_tot)
-        target = max((mu_aff / mu_c) ** 3 * mu_c, MU_FLOOR * gscale * hscale)
+        target = max((mu_aff / mu_c) ** SIGMA_POW * mu_c, MU_FLOOR * gscale * hscale)
         dU, ds, dl = newton(-s * lam - ds * dl + target)
         ap = min(1.0, TAU * _max_step(s, ds))
         ad = min(1.0, TAU * _max_step(lam, dl))
