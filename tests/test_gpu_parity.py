@@ -458,6 +458,27 @@ def test_interior_point_throughput_layout():
         assert rel_err_u0(U[b], Us[j].astype(np.float64)) < TOL_ACHIEVED_IPM, b
 
 
+def test_interior_point_standing_fleet_tail():
+    """Config 4's synthetic fleet all standing (2 048 robots, the bench's `--standing-every 1`
+    batch): every status OK, no robot above 18 factorisations (round 6: the Tapia polish set,
+    two corrections after an interior-point polish and the 0.98 step fraction; the slowest
+    robots of this batch took 22 and 21 before), and those two robots plus a sample against
+    the oracle."""
+    from mpcqp.synthetic import make_batch
+    N = 16
+    bt = make_batch(2048, N, seed=1000, gaits=("trot10", "pace10", "bound8"), robots=("a1",))
+    bt["contact"][:] = 1.0
+    eng = _engine(N)
+    eng.set_stance_range(4 * N, 4 * N)
+    u0, U, status, iters = _solve(eng, bt)
+    assert (status == 0).all(), np.unique(status, return_counts=True)
+    assert iters.max() <= 18, (int(iters.max()), int(np.argmax(iters)))
+    assert iters.mean() < 11.5, iters.mean()
+    for b in (1083, 231, 0, 1024, 2047):
+        x, _, _ = oracle_solution(bt, b, N)
+        assert max(rel_err_u0(u0[b], x[:12]), rel_err_u0(U[b], x)) < TOL_ACHIEVED_IPM, b
+
+
 def test_queue_set_eviction_beyond_eight_streams():
     """A context keeps queues for 8 streams; solves round-robin over 11 streams make the
     9th-11th take over the least recently used sets (after waiting on their last solve's
