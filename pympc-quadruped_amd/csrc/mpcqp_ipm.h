@@ -14,12 +14,14 @@
 //   * a Mehrotra predictor-corrector interior point whose Newton systems
 //     (H + G^T D G) d = rhs are solved by a Riccati recursion over the N stages,
 //     in information form: E_k = B W_k B^T (W_k = per-leg 3x3 (Rh + G^T D G)^-1),
-//     S_k = (I + P_{k+1} E_k)^-1 P_{k+1} (Gauss-Jordan on [I + P E | P]),
-//     P_k = Qh + A^T S_k A.  (The textbook P - P B (R + B^T P B)^-1 B^T P loses ~4
+//     S_k = (I + P_{k+1} E_k)^-1 P_{k+1}, P_k = Qh + A^T S_k A -- evaluated on B_d's
+//     6-dimensional range in the basis T = I - Nm / 2 (a 6-pivot Gauss-Jordan per stage,
+//     factor() below).  (The textbook P - P B (R + B^T P B)^-1 B^T P loses ~4
 //     digits: B_d has a 6-dimensional null space -- internal forces between feet --
 //     where only Rh = 2e-5 acts.)  The constant gravity state x[12] never moves in a
 //     Newton direction, so the recursions run on the 12-dimensional state.
-//   * an active-set polish: once mu is small, the rows with lambda > s define an
+//   * an active-set polish: once mu is small, the rows the last step moved towards
+//     activity (Tapia's indicator lambda+ / lambda > s+ / s) define an
 //     equality-constrained QP, solved exactly on each foot's null space (Gram-Schmidt
 //     of its active rows; the same Riccati with B_leg W_j B_leg^T, W_j = P_j (P_j Rh P_j
 //     + I - P_j)^-1 P_j) plus two Newton refinements, then verified: stationarity on
