@@ -1069,19 +1069,31 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     stage_weights(true);
     factor();
     ++nfact;
+    bool have_gr = false;   // sm.gr is the gradient at the final U (a refinement found it stationary)
     for (int rf = 0; rf < IPM_NREF; ++rf) {
       gradient();
       for (int e = lane; e < N * NU; e += NT) sm.rhs[e / NU][e % NU] = 0.0;
       fsync<NT>();
+      double st = 0.0;
       for (int j = lane; j < S; j += NT) {
         double g[3];
         foot(j, sm.gr, g);
         const double (&pj)[9] = FPJ(j);
         double* r = foot_ptr(j, sm.rhs);
 #pragma unroll
-        for (int x = 0; x < 3; ++x) r[x] = -(pj[3 * x] * g[0] + pj[3 * x + 1] * g[1] + pj[3 * x + 2] * g[2]);
+        for (int x = 0; x < 3; ++x) {
+          r[x] = -(pj[3 * x] * g[0] + pj[3 * x + 1] * g[1] + pj[3 * x + 2] * g[2]);
+          st = fmax(st, fabs(r[x]));
+        }
       }
       fsync<NT>();
+      // a later refinement of an already stationary iterate changes nothing the check can see:
+      // the check takes this gradient (round 6: one Newton solve and one gradient fewer per
+      // standing robot, tools/ipm_proto.py ADAPT_REF=1)
+      if (rf > 0 && sgpr_d(wave_max_d(st)) < IPM_STAT_TOL * gscale) {
+        have_gr = true;
+        break;
+      }
       lsolve();
       for (int j = lane; j < S; j += NT) {
         double d[3];
@@ -1093,7 +1105,7 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
       }
       fsync<NT>();
     }
-    gradient();
+    if (!have_gr) gradient();
     double stat = 0.0, smin = INFINITY, lminw = INFINITY;
     for (int j = lane; j < S; j += NT) {
       double g[3], f[3];

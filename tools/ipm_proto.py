@@ -35,6 +35,7 @@ MU_FLOOR = float(os.environ.get("MU_FLOOR", "1e-13"))   # centring target floor
 NREF = int(os.environ.get("NREF", "2"))                 # Newton refinements in the polish
 NCORR = int(os.environ.get("NCORR", "8"))               # active-set corrections per polish
 STAT_TOL = float(os.environ.get("STAT_TOL", "1e-10"))
+ADAPT_REF = int(os.environ.get("ADAPT_REF", "0"))       # 1: skip a refinement once stationary
 EARLY_CHG = int(os.environ.get("EARLY_CHG", "1000000"))  # give up once a correction changes more rows
 EARLY_MAXV = int(os.environ.get("EARLY_MAXV", "1000000"))  # only when the start violates <= this many rows
 EARLY = int(os.environ.get("EARLY", "-1"))              # >= 0: polish from the start point's violated
@@ -215,9 +216,15 @@ def solve(Ad, Bd, x0, xref, contact, N, mu, fz_max, normal, q_diag=F.Q_DIAG, r_d
             return np.concatenate([np.einsum("kij,kj->ki", Pi[:, l], v[:, 3 * l:3 * l + 3])
                                    for l in range(4)], axis=1)
 
-        for _ in range(NREF):
-            u = u + lsolve(Bl, Ri, S, -proj(gradient(u)))
-        gr = gradient(u)
+        gr = None
+        for rf in range(NREF):
+            g_ = gradient(u)
+            if rf > 0 and ADAPT_REF and np.abs(proj(g_)).max() < STAT_TOL * gscale:
+                gr = g_   # already stationary: the check takes this gradient
+                break
+            u = u + lsolve(Bl, Ri, S, -proj(g_))
+        if gr is None:
+            gr = gradient(u)
         stat = np.abs(proj(gr)).max()
         slack = fview(u) @ G.T - h
         lmin, drop = np.inf, np.zeros_like(act)
