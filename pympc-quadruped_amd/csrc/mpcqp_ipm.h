@@ -1220,9 +1220,15 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
   // ------------------------------------------------ interior point
   int it = 0;
   double ap_last = 0.0, ad_last = 0.0;   // the last step's lengths (FDS / FDL hold its direction); 0: none yet
+  // sm.gr after a step: g + ap H dU, H dU = rhs - G^T D G dU per foot-step (the Newton system
+  // (H + G^T D G) dU = rhs), in place of a forward simulation and adjoint per iteration
+  // (round 6, tools/ipm_proto.py INCR_GRAD=1: same iterations on its 64 cases, gradients per
+  // golden N = 16 robot 13.1 -> 4.4); any polish recomputes it from scratch
+  bool gr_valid = false;
   while (!done && it < IPM_MAX_IT) {
     ++it;
-    gradient();
+    if (!gr_valid) gradient();
+    gr_valid = false;
     // residuals rd = g - G^T lam, rp = G f - h - s; mu
     double sl = 0.0;
     for (int j = lane; j < S; j += NT) {
@@ -1255,7 +1261,9 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     dbg(gscale);
     dbg(hscale);
 #endif
+    bool polished = false;   // a failed polish left sm.gr at its own iterate
     if (mu < IPM_POLISH_MU * gscale * hscale) {
+      polished = true;
       for (int j = lane; j < S; j += NT) {
         int a = 0;
 #pragma unroll
@@ -1358,20 +1366,33 @@ __device__ __forceinline__ void solve_robot_ipm(const KParams& KP, int b, IpmSha
     ap_last = ap;
     ad_last = ad;
     for (int j = lane; j < S; j += NT) {
-      double d[3];
+      double d[3], rr[3];
       foot(j, sm.dU, d);
+      foot(j, sm.rhs, rr);   // the corrector's right-hand side
       double* u = foot_ptr(j, sm.U);
       u[0] += ap * d[0];
       u[1] += ap * d[1];
       u[2] += ap * d[2];
+      double* g = foot_ptr(j, sm.gr);
+      double hd[3] = {rr[0], rr[1], rr[2]};   // H d = rhs - G^T D G d (D of this iteration)
 #pragma unroll
       for (int r = 0; r < 6; ++r)
         if ((liv >> r) & 1) {
+          const double w = FL(j)[r] / FS(j)[r] * adot(r, d);
+          hd[0] = fma(-w, rw[r][0], hd[0]);
+          hd[1] = fma(-w, rw[r][1], hd[1]);
+          hd[2] = fma(-w, rw[r][2], hd[2]);
           FS(j)[r] += ap * FDS(j)[r];
           FL(j)[r] += ad * FDL(j)[r];
         }
+      if (!polished) {
+        g[0] = fma(ap, hd[0], g[0]);
+        g[1] = fma(ap, hd[1], g[1]);
+        g[2] = fma(ap, hd[2], g[2]);
+      }
     }
     fsync<NT>();
+    gr_valid = !polished;
   }
 
   // ------------------------------------------------ output (the polished optimum or the last iterate)

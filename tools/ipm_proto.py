@@ -36,6 +36,7 @@ NREF = int(os.environ.get("NREF", "2"))                 # Newton refinements in 
 NCORR = int(os.environ.get("NCORR", "8"))               # active-set corrections per polish
 STAT_TOL = float(os.environ.get("STAT_TOL", "1e-10"))
 ADAPT_REF = int(os.environ.get("ADAPT_REF", "0"))       # 1: skip a refinement once stationary
+INCR_GRAD = int(os.environ.get("INCR_GRAD", "0"))       # 1: IPM gradient updated by H dU = rhs - G^T D G dU
 EARLY_CHG = int(os.environ.get("EARLY_CHG", "1000000"))  # give up once a correction changes more rows
 EARLY_MAXV = int(os.environ.get("EARLY_MAXV", "1000000"))  # only when the start violates <= this many rows
 EARLY = int(os.environ.get("EARLY", "-1"))              # >= 0: polish from the start point's violated
@@ -286,8 +287,10 @@ def solve(Ad, Bd, x0, xref, contact, N, mu, fz_max, normal, q_diag=F.Q_DIAG, r_d
     lam = np.ones((nf, R))
     polish_tries = 0
     s_prev, lam_prev = None, None
+    g_inc = None
     for it in range(1, MAX_IT + 1):
-        rd = gradient(U) - gt(lam)
+        g_cur = g_inc if (INCR_GRAD and g_inc is not None) else gradient(U)
+        rd = g_cur - gt(lam)
         rp = fview(U) @ G.T - h - s
         mu_c = float((s * lam).sum() / m_tot)
         if verbose:
@@ -313,8 +316,10 @@ def solve(Ad, Bd, x0, xref, contact, N, mu, fz_max, normal, q_diag=F.Q_DIAG, r_d
         S = factor(Bl, Ri)
 
         def newton(rc):
-            dU = lsolve(Bl, Ri, S, -rd + gt(rc / s - D * rp))
+            rhs = -rd + gt(rc / s - D * rp)
+            dU = lsolve(Bl, Ri, S, rhs)
             ds = fview(dU) @ G.T + rp
+            newton.hd = rhs - gt(D * (fview(dU) @ G.T))   # H dU
             return dU, ds, (rc - lam * ds) / s
 
         dU, ds, dl = newton(-s * lam)
@@ -325,6 +330,7 @@ def solve(Ad, Bd, x0, xref, contact, N, mu, fz_max, normal, q_diag=F.Q_DIAG, r_d
         ap = min(1.0, TAU * _max_step(s, ds))
         ad = min(1.0, TAU * _max_step(lam, dl))
         U = U + ap * dU
+        g_inc = g_cur + ap * newton.hd
         s_prev, lam_prev = s, lam
         s = s + ap * ds
         lam = lam + ad * dl
